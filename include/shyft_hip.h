@@ -1,0 +1,146 @@
+/* shyft_hip.h — C ABI of the MI355X (gfx950) region engine.
+ *
+ * This is the drop-in boundary for Shyft's distributed-cell hot path:
+ * region_model::run_interpolation / run_cells (core/region_model.h:546-597)
+ * and the catchment statistics that consume run_cells' output
+ * (core/cell_model.h:228-368, api/api.h:289-318). The C++ host class that
+ * keeps the reference's region_model<cell_t> API (shyft_amd/csrc/host/) and
+ * the Python surface (shyft_amd.api) call nothing but these functions.
+ *
+ * Conventions
+ *  - Every function returns 0 on success, non-zero on error; the message is
+ *    available from shyft_hip_last_error(h) (or shyft_hip_last_error(NULL) for
+ *    errors raised before a handle exists). This replaces the std::runtime_error
+ *    the reference throws (region_model.h:583-592, cell_model.h:198-211).
+ *  - Cells are indexed 0..n_cells-1 in the caller's order. Host arrays are
+ *    borrowed for the duration of the call; device memory is owned by the handle.
+ *  - Time is int64 microseconds since 1970-01-01Z, as the reference's utctime
+ *    (core/utctime_utilities.h:29-34). The time axis is fixed_dt
+ *    (core/time_axis.h:74-115).
+ *  - Arrays marked [A][B] are row-major: element (a, b) at a*B + b.
+ */
+#ifndef SHYFT_HIP_H
+#define SHYFT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct shyft_hip_region shyft_hip_region;
+
+/* method stacks (core/pt_gs_k.h, core/hbv_stack.h, core/pt_ss_k.h) */
+enum shyft_hip_stack { SHYFT_HIP_PT_GS_K = 1, SHYFT_HIP_HBV_STACK = 2, SHYFT_HIP_PT_SS_K = 3 };
+
+/* forcing variables, the cell env_ts of core/cell_model.h:47-81 */
+enum shyft_hip_forcing {
+    SHYFT_HIP_TEMPERATURE = 0, SHYFT_HIP_PRECIPITATION = 1, SHYFT_HIP_WIND_SPEED = 2,
+    SHYFT_HIP_REL_HUM = 3, SHYFT_HIP_RADIATION = 4
+};
+
+/* response collection (core/pt_gs_k_cell_model.h:41-150):
+ *  DISCHARGE      = discharge_collector (avg_discharge, charge_m3s)
+ *  DISCHARGE_SNOW = discharge_collector with collect_snow (+ snow_sca, snow_swe)
+ *  ALL            = all_response_collector (8 series) */
+enum shyft_hip_collect { SHYFT_HIP_COLLECT_DISCHARGE = 0, SHYFT_HIP_COLLECT_DISCHARGE_SNOW = 1, SHYFT_HIP_COLLECT_ALL = 2 };
+
+/* pt_gs_k response series ids (all_response_collector member order) */
+enum shyft_hip_ptgsk_series {
+    SHYFT_HIP_AVG_DISCHARGE = 0, SHYFT_HIP_CHARGE_M3S = 1, SHYFT_HIP_SNOW_SCA = 2, SHYFT_HIP_SNOW_SWE = 3,
+    SHYFT_HIP_SNOW_OUTFLOW = 4, SHYFT_HIP_GLACIER_MELT = 5, SHYFT_HIP_AE_OUTPUT = 6, SHYFT_HIP_PE_OUTPUT = 7
+};
+
+/* statistics scope (core/cell_model.h:183-186 stat_scope) */
+enum shyft_hip_stat_scope { SHYFT_HIP_SCOPE_CELL_IX = 0, SHYFT_HIP_SCOPE_CATCHMENT = 1 };
+
+const char* shyft_hip_last_error(const shyft_hip_region* h);
+
+/* Replaces region_model(const vector<geo_cell_data>&, const parameter_t&) — core/region_model.h:285-293.
+ * device < 0 selects the current HIP device. */
+int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_region** out);
+void shyft_hip_region_destroy(shyft_hip_region* h);
+size_t shyft_hip_region_size(const shyft_hip_region* h);
+
+/* Cell geometry, n_cells x 11 doubles in the geo_cell_data_io layout
+ * (api/api.h:1598-1621): x y z area cid slope glacier lake reservoir forest unspecified.
+ * routing_id / routing_distance (geo_cell_data.routing, core/geo_cell_data.h:83-92) may be NULL. */
+int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* routing_id, const double* routing_distance);
+
+/* Parameters: n_sets rows of the stack's calibration vector in the reference's
+ * get/set order (pt_gs_k: 31 values, core/pt_gs_k.h:77-112); set_ix[n_cells]
+ * selects the row of each cell (region parameter + catchment overrides,
+ * region_model.h:287-319). set_ix == NULL means row 0 for every cell. */
+int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n_sets, size_t n_per_set,
+                             const int32_t* set_ix);
+
+/* Time axis (fixed_dt). Allocates forcing/response storage for a resident
+ * window of window_steps steps starting at step 0 (window_steps == 0: whole axis).
+ * Replaces initialize_cell_environment (region_model.h:359-364): forcing is NaN-filled. */
+int shyft_hip_set_time_axis(shyft_hip_region* h, int64_t t0_us, int64_t dt_us, size_t n_steps, size_t window_steps);
+/* Move the resident window to start at step w0 (window length unchanged). Forcing
+ * in the window becomes NaN, responses NaN. Used to stream long horizons in chunks. */
+int shyft_hip_set_window(shyft_hip_region* h, size_t w0);
+
+/* Collection mode (shyft_hip_collect) and state collection on/off
+ * (set_state_collection / set_snow_sca_swe_collection, region_model.h:784-818). */
+int shyft_hip_set_collection(shyft_hip_region* h, int collect, int collect_state);
+
+/* Catchment calculation filter (region_model.h:715-779): cids[n] or n == 0 to clear. */
+int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, size_t n);
+
+/* State, n_cells x n_fields (pt_gs_k: 9 = gs albedo lwc surface_heat alpha sdc_melt_mean acc_melt
+ * iso_pot_energy temp_swe, kirchner q). get/set_states (region_model.h:784-805). */
+int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_fields);
+int shyft_hip_get_state(const shyft_hip_region* h, double* state, size_t n_fields);
+
+/* Forcing for steps [step0, step0+n) of one variable, [n][n_cells].
+ * src_on_device != 0: src is a device pointer on the region's device. */
+int shyft_hip_set_forcing(shyft_hip_region* h, int var, size_t step0, size_t n, const double* src, int src_on_device);
+int shyft_hip_get_forcing(const shyft_hip_region* h, int var, size_t step0, size_t n, double* dst, int dst_on_device);
+
+/* Deterministic synthetic forcing for steps [step0, step0+n) of the resident window,
+ * generated on device (bench/test workload; SURVEY.md §8d generator). */
+int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n);
+/* The synthetic region's cell elevations z[i] = 2000*u(seed, 7, cell_offset+i, 0) (same generator), n_cells values. */
+int shyft_hip_synthetic_elevation(uint64_t seed, uint64_t cell_offset, size_t n_cells, double* z_host);
+
+/* region_model::run_cells(use_ncore, start_step, n_steps) — region_model.h:578-597.
+ * use_ncore is validated like the reference and otherwise ignored. Blocks until done. */
+int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps);
+/* Asynchronous variant on the region's stream (no argument re-validation of state). */
+int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps);
+int shyft_hip_synchronize(shyft_hip_region* h);
+/* Milliseconds of the last run_cells kernel launch(es), timed with HIP events on the region's stream. */
+double shyft_hip_last_run_ms(const shyft_hip_region* h);
+
+/* Response series for steps [step0, step0+n), [n][n_cells]. */
+int shyft_hip_get_series(const shyft_hip_region* h, int series, size_t step0, size_t n, double* dst, int dst_on_device);
+/* State-collector series (instant, T+1 axis), field f in state order, steps [step0, step0+n). */
+int shyft_hip_get_state_series(const shyft_hip_region* h, int field, size_t step0, size_t n, double* dst,
+                               int dst_on_device);
+
+/* Catchment statistics (cell_statistics::sum_catchment_feature / average_catchment_feature,
+ * core/cell_model.h:228-333): sum (weighted == 0) or area-weighted average (weighted != 0)
+ * of series `series` over the cells selected by ids[n_ids] (scope: cell index or catchment id;
+ * n_ids == 0 selects all cells), for steps [step0, step0+n). dst[n]. Throws (returns error)
+ * on unknown ids like verify_cids_exist (cell_model.h:198-211). */
+int shyft_hip_statistics(const shyft_hip_region* h, int series, const int64_t* ids, size_t n_ids, int scope,
+                         int weighted, size_t step0, size_t n, double* dst);
+/* Per-catchment sums of a series for all catchments at once (region_model::catchment_discharges,
+ * region_model.h:873-885): dst[n_catchments][n] in catchment_ids() order, device or host. */
+int shyft_hip_catchment_sums(const shyft_hip_region* h, int series, size_t step0, size_t n, double* dst,
+                             int dst_on_device);
+size_t shyft_hip_number_of_catchments(const shyft_hip_region* h);
+int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids);
+
+/* Diagnostic: evaluate one device elementary function (0 exp, 1 log, 2 pow(x, y), 3 lgamma,
+ * 4 gamma_p(x, y)) on n host inputs on the current device; out[n] host. Used by the parity
+ * tests to show device math == host math bit for bit. */
+int shyft_hip_math_selftest(int fn, const double* x, const double* y, size_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHYFT_HIP_H */

@@ -1,0 +1,22 @@
+// ORACLE — test infrastructure only (see common.hpp header).
+//
+// Elementary functions used by the restatement. Default: detmath (the
+// deterministic library the HIP kernels also use, detmath/detmath.h), so the
+// oracle is a bit-exact checker for the GPU path. Built with -DORACLE_LIBM the
+// oracle uses the host libm instead, as the reference build does; tests compare
+// the two variants to bound the effect of the elementary-function library.
+#pragma once
+#include <cmath>
+
+#ifdef ORACLE_LIBM
+#define OEXP(x) std::exp(x)
+#define OLOG(x) std::log(x)
+#define OPOW(x, y) std::pow(x, y)
+#define OLGAMMA(x) std::lgamma(x)
+#else
+#include "../../detmath/detmath.h"
+#define OEXP(x) detmath::exp(x)
+#define OLOG(x) detmath::log(x)
+#define OPOW(x, y) detmath::pow((double)(x), (double)(y))
+#define OLGAMMA(x) detmath::lgamma(x)
+#endif

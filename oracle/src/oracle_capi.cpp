@@ -1,0 +1,147 @@
+// ORACLE — test infrastructure only (see common.hpp header).
+//
+// C entry points of the CPU restatement, loaded by tests/ (ctypes) and by
+// bench.py's cpu_baseline leg. Not linked by the product library.
+#include <chrono>
+#include <cstring>
+#include <exception>
+
+#include "common.hpp"
+#include "methods.hpp"
+#include "ptgsk.hpp"
+#include "region.hpp"
+
+using namespace oracle;
+
+namespace {
+int fail(char* err, size_t errlen, const char* msg) {
+    if (err && errlen) {
+        std::strncpy(err, msg, errlen - 1);
+        err[errlen - 1] = 0;
+    }
+    return 1;
+}
+}  // namespace
+
+extern "C" {
+
+double oracle_gamma_p(double a, double x) { return special::gamma_p(a, x); }
+// the elementary functions this build uses (detmath, or libm with -DORACLE_LIBM)
+double oracle_exp(double x) { return OEXP(x); }
+double oracle_log(double x) { return OLOG(x); }
+double oracle_pow(double x, double y) { return OPOW(x, y); }
+double oracle_lgamma_fn(double x) { return OLGAMMA(x); }
+double oracle_lgamma(double a) { return special::lgamma_(a); }
+
+void oracle_gs_calc_snow_state(double shape, double scale, double y0, double lambda, double lwd, double max_water_frac,
+                               double temp_swe, double* swe, double* sca) {
+    gamma_snow::calculator gs;
+    gs.calc_snow_state(shape, scale, y0, lambda, lwd, max_water_frac, temp_swe, *swe, *sca);
+}
+
+double oracle_gs_corr_lwc(double z1, double a1, double b1, double z2, double a2, double b2) {
+    gamma_snow::calculator gs;
+    return gs.corr_lwc(z1, a1, b1, z2, a2, b2);
+}
+
+// state: 8 doubles (gamma_snow::state order), resp: sca, storage, outflow
+// gsp: the gamma_snow part given as a full 31-element pt_gs_k parameter vector
+int oracle_gs_step(double* st, double* resp, int64_t t_us, int64_t dt_us, const double* p31, double T, double rad,
+                   double prec, double ws, double rh, double forest, double altitude) {
+    pt_gs_k::parameter p;
+    p.set(p31);
+    gamma_snow::state s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+    gamma_snow::response r;
+    try {
+        gamma_snow::calculator().step(s, r, t_us, dt_us, p.gs, T, rad, prec, ws, rh, forest, altitude);
+    } catch (...) {
+        return 1;
+    }
+    st[0] = s.albedo; st[1] = s.lwc; st[2] = s.surface_heat; st[3] = s.alpha; st[4] = s.sdc_melt_mean;
+    st[5] = s.acc_melt; st[6] = s.iso_pot_energy; st[7] = s.temp_swe;
+    resp[0] = r.sca; resp[1] = r.storage; resp[2] = r.outflow;
+    return 0;
+}
+
+int oracle_kirchner_step(double c1, double c2, double c3, double abs_err, double rel_err, int64_t T0_us, int64_t T1_us,
+                         double* q, double* q_avg, double p, double e) {
+    kirchner::parameter kp{c1, c2, c3};
+    kirchner::calculator k(abs_err, rel_err, kp);
+    try {
+        k.step(T0_us, T1_us, *q, *q_avg, p, e);
+    } catch (...) {
+        return 1;
+    }
+    return 0;
+}
+
+double oracle_pt_pot_evap(double albedo, double alpha, double T, double rad, double rh) {
+    return priestley_taylor::calculator(albedo, alpha).potential_evapotranspiration(T, rad, rh);
+}
+
+int oracle_day_of_year(int64_t t_us) { return day_of_year(t_us); }
+int64_t oracle_trim_year(int64_t t_us) { return trim_year(t_us); }
+
+// Run the pt_gs_k region model on the CPU with the reference scheduler.
+//  geo11     : n_cells x 11 (geo_cell_data_io layout, api/api.h:1598-1621)
+//  params    : n_sets x 31 (pt_gs_k.h:77-112 order); set_ix[n_cells] selects a set per cell
+//  state     : n_cells x 9 in/out (pt_gs_k::state order, ptgsk.hpp)
+//  forcing   : five [T][n_cells] arrays (temperature, precipitation, wind_speed, rel_hum, radiation)
+//  out_main  : [2][T][n_cells] avg_discharge, charge_m3s (may be null)
+//  out_full  : [8][T][n_cells] all_response_collector series (may be null)
+//  out_state : [9][T+1][n_cells] state_collector series (may be null)
+//  elapsed_s : wall seconds spent in run_cells only
+int oracle_ptgsk_run(size_t n_cells, const double* geo11, const double* params, size_t n_sets, const int32_t* set_ix,
+                     double* state, int64_t t0_us, int64_t dt_us, size_t T, int start_step, int n_steps, const double* temp,
+                     const double* prec, const double* ws, const double* rh, const double* rad, double* out_main,
+                     double* out_full, double* out_state, int ncore, double* elapsed_s, char* err, size_t errlen) {
+    try {
+        ptgsk_region rm;
+        rm.time_axis = fixed_dt(t0_us, dt_us, T);
+        rm.params.resize(n_sets);
+        for (size_t k = 0; k < n_sets; ++k) rm.params[k].set(params + k * 31);
+        rm.cells.resize(n_cells);
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.geo = geo_cell_data::from_raw(geo11 + i * 11);
+            int32_t k = set_ix ? set_ix[i] : 0;
+            if (k < 0 || size_t(k) >= n_sets) return fail(err, errlen, "oracle_ptgsk_run: parameter set index out of range");
+            c.parameter = &rm.params[k];
+            c.state.set(state + i * 9);
+            c.temp.resize(T); c.prec.resize(T); c.ws.resize(T); c.rh.resize(T); c.rad.resize(T);
+            for (size_t t = 0; t < T; ++t) {
+                c.temp[t] = temp[t * n_cells + i];
+                c.prec[t] = prec[t * n_cells + i];
+                c.ws[t] = ws[t * n_cells + i];
+                c.rh[t] = rh[t * n_cells + i];
+                c.rad[t] = rad[t * n_cells + i];
+            }
+            c.col.full = out_full != nullptr;
+            c.col.collect_state = out_state != nullptr;
+        }
+        auto t_begin = std::chrono::steady_clock::now();
+        rm.run_cells(size_t(ncore < 0 ? 0 : ncore), start_step, n_steps);
+        auto t_end = std::chrono::steady_clock::now();
+        if (elapsed_s) *elapsed_s = std::chrono::duration<double>(t_end - t_begin).count();
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.state.get(state + i * 9);
+            for (size_t t = 0; t < T; ++t) {
+                if (out_main) {
+                    out_main[t * n_cells + i] = c.col.rc[pt_gs_k::AVG_DISCHARGE][t];
+                    out_main[(T + t) * n_cells + i] = c.col.rc[pt_gs_k::CHARGE_M3S][t];
+                }
+                if (out_full)
+                    for (int k = 0; k < pt_gs_k::N_ALL; ++k) out_full[(size_t(k) * T + t) * n_cells + i] = c.col.rc[k][t];
+            }
+            if (out_state)
+                for (int k = 0; k < 9; ++k)
+                    for (size_t t = 0; t <= T; ++t) out_state[(size_t(k) * (T + 1) + t) * n_cells + i] = c.col.sc[k][t];
+        }
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
+}  // extern "C"

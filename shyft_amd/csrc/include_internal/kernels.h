@@ -1,0 +1,48 @@
+// Kernel argument structs and launch entry points (internal to libshyft_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.h"
+
+struct ptgsk_kargs {
+    int n_cells;      // lanes (cells) in the launch
+    int step0;        // first absolute step to run
+    int n_steps;      // number of steps
+    int win0;         // absolute step of window row 0
+    int win_len;      // window rows (forcing/response stride)
+    int collect;      // collect_mode
+    double dt_s;      // to_seconds(dt)
+    double dt_us;     // dt in microseconds (as double)
+    double t1_hours;  // kirchner integration end: to_seconds(dt)/3600
+    const int32_t* doy;            // [T] day of year of period start
+    const int64_t* t_rel_year_us;  // [T] period start - trim(start, YEAR)
+    const double* params;          // [n_sets][PTGSK_NP]
+    const int32_t* set_ix;         // [N]
+    const double* cellc;           // [PTGSK_NC][N]
+    double* state;                 // [PTGSK_NS][N]
+    const double* forcing;         // [N_FORCING][win_len][N]
+    double* resp;                  // [n_series][win_len][N]
+    double* state_series;          // [PTGSK_NS][win_len+1][N] or null
+    const uint8_t* active;         // [N] catchment filter or null
+    int32_t* err;                  // [N]
+};
+
+hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream);
+
+// synthetic workload generator, fills [5][n][N] window rows
+hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
+                                    uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
+                                    hipStream_t stream);
+
+// sums over selected cells: out[t] = sum_k w[k]*series[t][cells[k]] for t in [0,n)
+// (w == null -> plain sum), deterministic fixed-order tree per step
+hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_steps, const int32_t* cells, size_t n_sel,
+                             const double* w, double* out, hipStream_t stream);
+
+// per-catchment sums: out[c][t] = sum over cells of segment c (seg_cells[seg_off[c]..seg_off[c+1]))
+hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
+                               const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream);
+
+// fill with a constant
+hipError_t launch_fill(double* p, size_t n, double v, hipStream_t stream);

@@ -1,0 +1,95 @@
+// Catchment statistics kernels (gfx950): the reductions behind
+// cell_statistics::sum_catchment_feature / average_catchment_feature
+// (core/cell_model.h:228-333) and region_model::catchment_discharges
+// (core/region_model.h:873-885).
+//
+// Series are [step][cell]. One workgroup reduces one step (and, for segment
+// sums, one catchment): lanes stride over the selected cells in a fixed order,
+// then a fixed-shape wavefront shuffle tree + LDS combine, so results are
+// bitwise reproducible run to run (no float atomics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../include_internal/kernels.h"
+
+namespace {
+
+constexpr int RB = 256;  // 4 wavefronts
+
+__device__ inline double wave_sum(double v) {
+    // fixed butterfly over 64 lanes
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ inline double block_sum(double v) {
+    __shared__ double part[RB / 64];
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) part[wid] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) {
+        r = part[0];
+        for (int w = 1; w < RB / 64; ++w) r += part[w];
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(RB) void select_sum_kernel(const double* __restrict__ series, size_t n_cells,
+                                                        const int32_t* __restrict__ cells, size_t n_sel,
+                                                        const double* __restrict__ w, double* __restrict__ out) {
+    const size_t t = blockIdx.x;
+    const double* __restrict__ row = series + t * n_cells;
+    double acc = 0.0;
+    if (w) {
+        for (size_t k = threadIdx.x; k < n_sel; k += RB) acc += row[cells[k]] * w[k];
+    } else {
+        for (size_t k = threadIdx.x; k < n_sel; k += RB) acc += row[cells[k]];
+    }
+    const double r = block_sum(acc);
+    if (threadIdx.x == 0) out[t] = r;
+}
+
+__global__ __launch_bounds__(RB) void segment_sum_kernel(const double* __restrict__ series, size_t n_cells, size_t n_steps,
+                                                         const int32_t* __restrict__ seg_cells,
+                                                         const int32_t* __restrict__ seg_off, double* __restrict__ out) {
+    const size_t t = blockIdx.x;
+    const size_t c = blockIdx.y;
+    const double* __restrict__ row = series + t * n_cells;
+    const int32_t b = seg_off[c], e = seg_off[c + 1];
+    double acc = 0.0;
+    for (int32_t k = b + (int32_t)threadIdx.x; k < e; k += RB) acc += row[seg_cells[k]];
+    const double r = block_sum(acc);
+    if (threadIdx.x == 0) out[c * n_steps + t] = r;
+}
+
+__global__ void fill_kernel(double* __restrict__ p, size_t n, double v) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+}  // namespace
+
+hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_steps, const int32_t* cells, size_t n_sel,
+                             const double* w, double* out, hipStream_t stream) {
+    if (n_steps == 0) return hipSuccess;
+    hipLaunchKernelGGL(select_sum_kernel, dim3((unsigned)n_steps), dim3(RB), 0, stream, series, n_cells, cells, n_sel, w,
+                       out);
+    return hipGetLastError();
+}
+
+hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
+                               const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream) {
+    if (n_steps == 0 || n_seg == 0) return hipSuccess;
+    hipLaunchKernelGGL(segment_sum_kernel, dim3((unsigned)n_steps, (unsigned)n_seg), dim3(RB), 0, stream, series, n_cells,
+                       n_steps, seg_cells, seg_off, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(double* p, size_t n, double v, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(fill_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, n, v);
+    return hipGetLastError();
+}

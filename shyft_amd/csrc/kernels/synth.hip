@@ -1,0 +1,42 @@
+// Deterministic synthetic forcing generator for the bench and
+// the parity tests. Integer hashing (SplitMix64) plus IEEE-exact + - * / only,
+// with FP contraction off, so numpy (shyft_amd/synthetic.py) reproduces every
+// value bit for bit on the host.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../include_internal/kernels.h"
+#include "../include_internal/synth_hash.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void synthetic_forcing_kernel(double* __restrict__ forcing, size_t win_len, size_t row0,
+                                                                size_t n_rows, size_t n_cells, uint64_t seed,
+                                                                uint64_t cell_offset, uint64_t step0,
+                                                                const double* __restrict__ zc) {
+#pragma clang fp contract(off)
+    const size_t cell = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (cell >= n_cells) return;
+    const double z = zc[cell];
+    const uint64_t gcell = cell_offset + cell;
+    for (size_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
+        const uint64_t step = step0 + r;
+        double v[5];
+        synth_values(seed, gcell, step, z, v);
+        const size_t o = (row0 + r) * n_cells + cell;
+        for (int k = 0; k < 5; ++k) forcing[(size_t)k * win_len * n_cells + o] = v[k];
+    }
+}
+
+}  // namespace
+
+hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
+                                    uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
+                                    hipStream_t stream) {
+    if (n_rows == 0 || n_cells == 0) return hipSuccess;
+    const unsigned gx = (unsigned)((n_cells + 255) / 256);
+    unsigned gy = (unsigned)(n_rows < 64 ? n_rows : 64);
+    hipLaunchKernelGGL(synthetic_forcing_kernel, dim3(gx, gy), dim3(256), 0, stream, forcing, win_len, row0, n_rows,
+                       n_cells, seed, cell_offset, step0, z);
+    return hipGetLastError();
+}

@@ -1,0 +1,713 @@
+// C-ABI implementation (include/shyft_hip.h): one region handle owns the
+// SoA device buffers of its cells on one device and one HIP stream.
+//
+// Mirrors the state machine of region_model (core/region_model.h:211-1049):
+// cells + parameters + time axis + cell environment (forcing) + state +
+// collectors; run_cells launches one kernel over every cell of the region.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/shyft_hip.h"
+#include "include_internal/kernels.h"
+#include "include_internal/layout.h"
+#include "include_internal/synth_hash.h"
+#include "../../detmath/detmath.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct hip_error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw hip_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+struct dbuf {
+    T* p = nullptr;
+    size_t n = 0;
+    dbuf() = default;
+    dbuf(const dbuf&) = delete;
+    dbuf& operator=(const dbuf&) = delete;
+    ~dbuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        if (count == n && p) return;
+        release();
+        if (count == 0) return;
+        hip_check(hipMalloc(&p, count * sizeof(T)), "hipMalloc");
+        n = count;
+    }
+};
+
+// UTC civil calendar (core/utctime_utilities.cpp:230-253)
+int64_t floor_div(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+    return q;
+}
+void civil_from_days(int64_t z, int64_t& y, int& m, int& d) {
+    z += 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    y = yoe + era * 400;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    d = int(doy - (153 * mp + 2) / 5 + 1);
+    m = int(mp < 10 ? mp + 3 : mp - 9);
+    y += (m <= 2);
+}
+int64_t days_from_civil(int64_t y, int m, int d) {
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+constexpr int64_t DAY_US = 86400LL * 1000000LL;
+
+}  // namespace
+
+struct shyft_hip_region {
+    int stack = 0;
+    size_t n = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    double last_ms = 0.0;
+
+    // host mirrors
+    std::vector<double> geo;  // n x 11
+    std::vector<int64_t> routing_id;
+    std::vector<double> routing_distance;
+    std::vector<int64_t> cid;          // per cell
+    std::vector<size_t> cix;           // per cell
+    std::vector<int64_t> cix_to_cid;   // region_model::cix_to_cid
+    std::map<int64_t, size_t> cid_to_cix;
+    std::vector<double> params;        // n_sets x n_ref
+    size_t n_sets = 0;
+    std::vector<int32_t> set_ix;
+    std::vector<uint8_t> active;       // empty = no filter
+    int64_t t0 = 0, dt = 0;
+    size_t T = 0, w0 = 0, TW = 0;
+    int collect = COLLECT_DISCHARGE;
+    int collect_state = 0;
+    bool derived_dirty = true;
+    bool has_geo = false, has_params = false, has_state = false;
+
+    // device
+    dbuf<double> d_params, d_cellc, d_state, d_forcing, d_resp, d_state_series;
+    dbuf<int32_t> d_set_ix, d_err, d_doy, d_seg_cells, d_seg_off, d_sel;
+    dbuf<int64_t> d_trel;
+    dbuf<uint8_t> d_active;
+    dbuf<double> d_tmp, d_w;
+    dbuf<int32_t> d_flag;
+
+    size_t n_series() const { return collect == COLLECT_ALL ? PTGSK_NR : (collect == COLLECT_DISCHARGE_SNOW ? 4 : 2); }
+    size_t n_state_fields() const { return PTGSK_NS; }
+    size_t n_ref_params() const { return PTGSK_NP_REF; }
+};
+
+namespace {
+
+int fail(shyft_hip_region* h, const std::string& msg) {
+    if (h) h->err = msg;
+    g_last_error = msg;
+    return 1;
+}
+
+template <class F>
+int guarded(shyft_hip_region* h, F&& f) {
+    try {
+        if (h) hip_check(hipSetDevice(h->device), "hipSetDevice");
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        return fail(h, e.what());
+    } catch (...) {
+        return fail(h, "unknown error");
+    }
+}
+
+// region_model::update_ix_to_id_mapping (region_model.h:236-252)
+void update_ix_to_id_mapping(shyft_hip_region* h) {
+    h->cid_to_cix.clear();
+    h->cix_to_cid.clear();
+    h->cid.resize(h->n);
+    h->cix.resize(h->n);
+    for (size_t i = 0; i < h->n; ++i) {
+        const int64_t c = int64_t(int(h->geo[i * 11 + 4]));
+        h->cid[i] = c;
+        auto f = h->cid_to_cix.find(c);
+        if (f == h->cid_to_cix.end()) {
+            h->cid_to_cix[c] = h->cix_to_cid.size();
+            h->cix[i] = h->cix_to_cid.size();
+            h->cix_to_cid.push_back(c);
+        } else {
+            h->cix[i] = f->second;
+        }
+    }
+    // catchment segments: cells of each catchment in cell order
+    const size_t C = h->cix_to_cid.size();
+    std::vector<int32_t> off(C + 1, 0), cells(h->n);
+    for (size_t i = 0; i < h->n; ++i) off[h->cix[i] + 1]++;
+    for (size_t c = 0; c < C; ++c) off[c + 1] += off[c];
+    std::vector<int32_t> pos(off.begin(), off.end() - 1);
+    for (size_t i = 0; i < h->n; ++i) cells[pos[h->cix[i]]++] = int32_t(i);
+    h->d_seg_cells.alloc(h->n);
+    h->d_seg_off.alloc(C + 1);
+    hip_check(hipMemcpy(h->d_seg_cells.p, cells.data(), h->n * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
+    hip_check(hipMemcpy(h->d_seg_off.p, off.data(), (C + 1) * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
+}
+
+// derived per-set parameter rows and per-cell constants (pt_gs_k.h:347-357,
+// gamma_snow.h:85-87, :188, :340-343). Evaluated with the same expressions
+// the reference evaluates, on the host.
+void update_derived(shyft_hip_region* h) {
+    if (!h->derived_dirty) return;
+    if (!h->has_geo) throw std::runtime_error("region: geo_cell_data not set");
+    if (!h->has_params) throw std::runtime_error("region: parameters not set");
+    if (h->dt <= 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
+    const size_t N = h->n;
+    const double dt_s = double(h->dt) / 1e6;
+    const double dt_in_days = dt_s / 86400.0;
+    std::vector<double> P(h->n_sets * PTGSK_NP, 0.0);
+    for (size_t k = 0; k < h->n_sets; ++k) {
+        const double* p = &h->params[k * PTGSK_NP_REF];
+        double* q = &P[k * PTGSK_NP];
+        for (int j = 0; j < PTGSK_NP_REF; ++j) q[j] = p[j];
+        q[PK_WED] = double(size_t(p[PK_WED]));   // size_t(p[i]) (pt_gs_k.h:103)
+        q[PK_NWD] = double(size_t(p[PK_NWD]));   // implicit size_t conversion (pt_gs_k.h:109)
+        q[PK_ISO] = p[PK_ISO] != 0.0 ? 1.0 : 0.0;
+        const double albedo_range = p[PK_MAX_ALBEDO] - p[PK_MIN_ALBEDO];
+        q[PK_ALBEDO_RANGE] = albedo_range;
+        q[PK_SLOW_DECAY] = 0.5 * albedo_range * dt_in_days / p[PK_SLOW_DECAY_RATE];
+        q[PK_FAST_DECAY] = detmath::pow(2.0, -dt_in_days / p[PK_FAST_DECAY_RATE]);
+        q[PK_BB0] = 0.98 * 5.670373e-8 * detmath::pow(273.15, 4.0);
+        q[PK_INV_CV2_PARAM] = 1.0 / (p[PK_SNOW_CV] * p[PK_SNOW_CV]);
+    }
+    std::vector<double> cc(PTGSK_NC * N);
+    for (size_t i = 0; i < N; ++i) {
+        const double* g = &h->geo[i * 11];
+        const double* p = &h->params[size_t(h->set_ix[i]) * PTGSK_NP_REF];
+        const double glacier = g[6], lake = g[7], reservoir = g[8], forest = g[9];
+        const double gm_direct = p[PK_GM_DIRECT];
+        const double rdrf = p[PK_RSV_DRF];
+        const double direct = glacier * gm_direct + reservoir * rdrf;
+        const double cv = p[PK_SNOW_CV] + forest * p[PK_CV_FOREST] + g[2] * p[PK_CV_ALT];
+        cc[PC_FOREST * N + i] = forest;
+        cc[PC_GLACIER * N + i] = glacier;
+        cc[PC_SNOW_STORAGE * N + i] = 1.0 - lake - reservoir;
+        cc[PC_KIRCHNER_ROUTED_PREC * N + i] = reservoir * (1.0 - rdrf) + lake;
+        cc[PC_DIRECT_RESPONSE * N + i] = direct;
+        cc[PC_KIRCHNER_FRACTION * N + i] = 1 - direct;
+        cc[PC_AREA * N + i] = g[3];
+        cc[PC_GLACIER_AREA * N + i] = g[3] * glacier;
+        cc[PC_ALTITUDE * N + i] = g[2];
+        cc[PC_CV2 * N + i] = cv * cv;
+        cc[PC_INV_CV2 * N + i] = 1.0 / (cv * cv);
+    }
+    h->d_params.alloc(P.size());
+    h->d_cellc.alloc(cc.size());
+    h->d_set_ix.alloc(N);
+    hip_check(hipMemcpy(h->d_params.p, P.data(), P.size() * sizeof(double), hipMemcpyHostToDevice), "upload params");
+    hip_check(hipMemcpy(h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
+    hip_check(hipMemcpy(h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
+    h->derived_dirty = false;
+}
+
+void alloc_window(shyft_hip_region* h) {
+    const size_t N = h->n;
+    h->d_forcing.alloc(N_FORCING * h->TW * N);
+    hip_check(launch_fill(h->d_forcing.p, h->d_forcing.n, NAN, h->stream), "fill forcing");
+    h->d_resp.alloc(h->n_series() * h->TW * N);
+    hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill resp");
+    if (h->collect_state) {
+        h->d_state_series.alloc(PTGSK_NS * (h->TW + 1) * N);
+        hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill state series");
+    } else {
+        h->d_state_series.release();
+    }
+    hip_check(hipStreamSynchronize(h->stream), "sync");
+}
+
+void check_window(const shyft_hip_region* h, size_t step0, size_t n, const char* what) {
+    if (step0 < h->w0 || step0 + n > h->w0 + h->TW)
+        throw std::runtime_error(std::string(what) + ": steps [" + std::to_string(step0) + "," + std::to_string(step0 + n) +
+                                 ") outside the resident window [" + std::to_string(h->w0) + "," +
+                                 std::to_string(h->w0 + h->TW) + ")");
+}
+
+void copy_rows(hipStream_t s, double* dst, const double* src, size_t bytes, int dst_dev, int src_dev) {
+    hipMemcpyKind k = src_dev ? (dst_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost)
+                              : (dst_dev ? hipMemcpyHostToDevice : hipMemcpyHostToHost);
+    hip_check(hipMemcpyAsync(dst, src, bytes, k, s), "hipMemcpyAsync");
+    hip_check(hipStreamSynchronize(s), "sync");
+}
+
+// cell_statistics::verify_cids_exist (cell_model.h:198-211) + is_match selection
+std::vector<int32_t> select_cells(const shyft_hip_region* h, const int64_t* ids, size_t n_ids, int scope) {
+    std::vector<int32_t> sel;
+    if (n_ids == 0) {
+        sel.resize(h->n);
+        for (size_t i = 0; i < h->n; ++i) sel[i] = int32_t(i);
+        return sel;
+    }
+    if (scope == SHYFT_HIP_SCOPE_CELL_IX) {
+        for (size_t k = 0; k < n_ids; ++k)
+            if (ids[k] < 0 || ids[k] > int64_t(h->n))
+                throw std::runtime_error("Supplied cell index reference " + std::to_string(ids[k]) +
+                                         " is ouside valid range 0 .." + std::to_string(h->n));
+        for (size_t i = 0; i < h->n; ++i)
+            for (size_t k = 0; k < n_ids; ++k)
+                if (ids[k] == int64_t(i)) { sel.push_back(int32_t(i)); break; }
+    } else {
+        for (size_t k = 0; k < n_ids; ++k)
+            if (h->cid_to_cix.count(ids[k]) == 0)
+                throw std::runtime_error("one or more supplied catchment_indexes does not exist:" + std::to_string(ids[k]));
+        for (size_t i = 0; i < h->n; ++i)
+            for (size_t k = 0; k < n_ids; ++k)
+                if (h->cid[i] == ids[k]) { sel.push_back(int32_t(i)); break; }
+    }
+    return sel;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* shyft_hip_last_error(const shyft_hip_region* h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+
+int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_region** out) {
+    if (!out) return fail(nullptr, "shyft_hip_region_create: out is null");
+    *out = nullptr;
+    if (stack != SHYFT_HIP_PT_GS_K) return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
+    if (n_cells == 0 || n_cells > (size_t)INT32_MAX) return fail(nullptr, "shyft_hip_region_create: invalid n_cells");
+    std::unique_ptr<shyft_hip_region> h(new shyft_hip_region());
+    h->stack = stack;
+    h->n = n_cells;
+    try {
+        if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
+        h->device = device;
+        hip_check(hipSetDevice(device), "hipSetDevice");
+        hip_check(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+        hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
+        hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
+        h->d_state.alloc(PTGSK_NS * n_cells);
+        h->d_err.alloc(n_cells);
+        h->d_flag.alloc(1);
+        hip_check(hipMemset(h->d_err.p, 0, n_cells * sizeof(int32_t)), "memset");
+        h->set_ix.assign(n_cells, 0);
+    } catch (const std::exception& e) {
+        return fail(nullptr, e.what());
+    }
+    *out = h.release();
+    return 0;
+}
+
+void shyft_hip_region_destroy(shyft_hip_region* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+size_t shyft_hip_region_size(const shyft_hip_region* h) { return h ? h->n : 0; }
+
+int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* routing_id, const double* routing_distance) {
+    if (!h || !geo11) return fail(h, "shyft_hip_set_geo: null argument");
+    return guarded(h, [&] {
+        for (size_t i = 0; i < h->n; ++i) {
+            const double* g = geo11 + i * 11;
+            // land_type_fractions::set_fractions validation (geo_cell_data.h:67-79)
+            const double sum = g[6] + g[7] + g[8] + g[9];
+            if (!(sum > 1.0 && sum < 1.0 + 1.0e-3) && (sum > 1.0 || g[6] < 0 || g[7] < 0 || g[8] < 0 || g[9] < 0))
+                throw std::invalid_argument("LandTypeFractions:: must be >=0.0 and sum <= 1.0");
+        }
+        h->geo.assign(geo11, geo11 + 11 * h->n);
+        for (size_t i = 0; i < h->n; ++i) {  // normalise like set_fractions
+            double* g = &h->geo[i * 11];
+            const double sum = g[6] + g[7] + g[8] + g[9];
+            if (sum > 1.0 && sum < 1.0 + 1.0e-3)
+                for (int k = 6; k < 10; ++k) g[k] /= sum;
+        }
+        h->routing_id.assign(h->n, 0);
+        h->routing_distance.assign(h->n, 0.0);
+        if (routing_id) h->routing_id.assign(routing_id, routing_id + h->n);
+        if (routing_distance) h->routing_distance.assign(routing_distance, routing_distance + h->n);
+        update_ix_to_id_mapping(h);
+        h->has_geo = true;
+        h->derived_dirty = true;
+    });
+}
+
+int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n_sets, size_t n_per_set,
+                             const int32_t* set_ix) {
+    if (!h || !params) return fail(h, "shyft_hip_set_parameters: null argument");
+    return guarded(h, [&] {
+        if (n_per_set != h->n_ref_params())
+            throw std::runtime_error("PTGSK Parameter Accessor: .set size missmatch");
+        if (n_sets == 0) throw std::runtime_error("shyft_hip_set_parameters: n_sets == 0");
+        std::vector<int32_t> ix(h->n, 0);
+        if (set_ix) {
+            for (size_t i = 0; i < h->n; ++i) {
+                if (set_ix[i] < 0 || size_t(set_ix[i]) >= n_sets)
+                    throw std::runtime_error("shyft_hip_set_parameters: set index out of range");
+                ix[i] = set_ix[i];
+            }
+        }
+        h->params.assign(params, params + n_sets * n_per_set);
+        h->n_sets = n_sets;
+        h->set_ix.swap(ix);
+        h->has_params = true;
+        h->derived_dirty = true;
+    });
+}
+
+int shyft_hip_set_time_axis(shyft_hip_region* h, int64_t t0_us, int64_t dt_us, size_t n_steps, size_t window_steps) {
+    if (!h) return fail(h, "shyft_hip_set_time_axis: null handle");
+    return guarded(h, [&] {
+        if (dt_us <= 0 || n_steps == 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
+        if (n_steps > (size_t)INT32_MAX) throw std::runtime_error("time axis too long");
+        h->t0 = t0_us;
+        h->dt = dt_us;
+        h->T = n_steps;
+        h->w0 = 0;
+        h->TW = (window_steps == 0 || window_steps > n_steps) ? n_steps : window_steps;
+        std::vector<int32_t> doy(n_steps);
+        std::vector<int64_t> trel(n_steps);
+        for (size_t i = 0; i < n_steps; ++i) {
+            const int64_t t = t0_us + int64_t(i) * dt_us;
+            const int64_t days = floor_div(t, DAY_US);
+            int64_t y; int m, d;
+            civil_from_days(days, y, m, d);
+            const int64_t jan1 = days_from_civil(y, 1, 1);
+            doy[i] = int32_t(1 + days - jan1);  // calendar::day_of_year
+            trel[i] = t - jan1 * DAY_US;        // t - calendar::trim(t, YEAR)
+        }
+        h->d_doy.alloc(n_steps);
+        h->d_trel.alloc(n_steps);
+        hip_check(hipMemcpy(h->d_doy.p, doy.data(), n_steps * sizeof(int32_t), hipMemcpyHostToDevice), "upload doy");
+        hip_check(hipMemcpy(h->d_trel.p, trel.data(), n_steps * sizeof(int64_t), hipMemcpyHostToDevice), "upload trel");
+        alloc_window(h);
+        h->derived_dirty = true;
+    });
+}
+
+int shyft_hip_set_window(shyft_hip_region* h, size_t w0) {
+    if (!h) return fail(h, "shyft_hip_set_window: null handle");
+    return guarded(h, [&] {
+        if (h->T == 0) throw std::runtime_error("set_window: no time axis");
+        if (w0 + h->TW > h->T) throw std::runtime_error("set_window: window beyond the time axis");
+        h->w0 = w0;
+        hip_check(launch_fill(h->d_forcing.p, h->d_forcing.n, NAN, h->stream), "fill");
+        hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill");
+        if (h->d_state_series.p) hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill");
+        hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_set_collection(shyft_hip_region* h, int collect, int collect_state) {
+    if (!h) return fail(h, "shyft_hip_set_collection: null handle");
+    return guarded(h, [&] {
+        if (collect < 0 || collect > 2) throw std::runtime_error("set_collection: invalid mode");
+        const bool changed = collect != h->collect || (collect_state != 0) != (h->collect_state != 0);
+        h->collect = collect;
+        h->collect_state = collect_state != 0;
+        if (changed && h->TW) {
+            const size_t N = h->n;
+            h->d_resp.alloc(h->n_series() * h->TW * N);
+            hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill resp");
+            if (h->collect_state) {
+                h->d_state_series.alloc(PTGSK_NS * (h->TW + 1) * N);
+                hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill");
+            } else {
+                h->d_state_series.release();
+            }
+            hip_check(hipStreamSynchronize(h->stream), "sync");
+        }
+    });
+}
+
+int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, size_t n) {
+    if (!h) return fail(h, "shyft_hip_set_catchment_filter: null handle");
+    return guarded(h, [&] {
+        if (n == 0) {
+            h->active.clear();
+            h->d_active.release();
+            return;
+        }
+        // region_model::set_catchment_calculation_filter (region_model.h:356-370)
+        if (n > h->cix_to_cid.size())
+            throw std::runtime_error("set_catchment_calculation_filter: supplied list > available catchments");
+        for (size_t k = 0; k < n; ++k)
+            if (h->cid_to_cix.find(cids[k]) == h->cid_to_cix.end())
+                throw std::runtime_error("set_catchment_calculation_filter: no cells have supplied cid");
+        std::vector<bool> cf(h->cix_to_cid.size(), false);
+        for (size_t k = 0; k < n; ++k) cf[h->cid_to_cix[cids[k]]] = true;
+        h->active.assign(h->n, 0);
+        for (size_t i = 0; i < h->n; ++i) h->active[i] = cf[h->cix[i]] ? 1 : 0;
+        h->d_active.alloc(h->n);
+        hip_check(hipMemcpy(h->d_active.p, h->active.data(), h->n, hipMemcpyHostToDevice), "upload filter");
+    });
+}
+
+int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_fields) {
+    if (!h || !state) return fail(h, "shyft_hip_set_state: null argument");
+    return guarded(h, [&] {
+        if (n_fields != h->n_state_fields()) throw std::runtime_error("set_state: wrong number of state fields");
+        const size_t N = h->n;
+        std::vector<double> soa(n_fields * N);
+        for (size_t i = 0; i < N; ++i)
+            for (size_t f = 0; f < n_fields; ++f) soa[f * N + i] = state[i * n_fields + f];
+        hip_check(hipMemcpy(h->d_state.p, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice), "upload state");
+        h->has_state = true;
+    });
+}
+
+int shyft_hip_get_state(const shyft_hip_region* hc, double* state, size_t n_fields) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !state) return fail(h, "shyft_hip_get_state: null argument");
+    return guarded(h, [&] {
+        if (n_fields != h->n_state_fields()) throw std::runtime_error("get_state: wrong number of state fields");
+        const size_t N = h->n;
+        std::vector<double> soa(n_fields * N);
+        hip_check(hipMemcpy(soa.data(), h->d_state.p, soa.size() * sizeof(double), hipMemcpyDeviceToHost), "download state");
+        for (size_t i = 0; i < N; ++i)
+            for (size_t f = 0; f < n_fields; ++f) state[i * n_fields + f] = soa[f * N + i];
+    });
+}
+
+int shyft_hip_set_forcing(shyft_hip_region* h, int var, size_t step0, size_t n, const double* src, int src_on_device) {
+    if (!h || !src) return fail(h, "shyft_hip_set_forcing: null argument");
+    return guarded(h, [&] {
+        if (var < 0 || var >= N_FORCING) throw std::runtime_error("set_forcing: invalid variable");
+        check_window(h, step0, n, "set_forcing");
+        double* dst = h->d_forcing.p + (size_t(var) * h->TW + (step0 - h->w0)) * h->n;
+        copy_rows(h->stream, dst, src, n * h->n * sizeof(double), 1, src_on_device);
+    });
+}
+
+int shyft_hip_get_forcing(const shyft_hip_region* hc, int var, size_t step0, size_t n, double* dst, int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_get_forcing: null argument");
+    return guarded(h, [&] {
+        if (var < 0 || var >= N_FORCING) throw std::runtime_error("get_forcing: invalid variable");
+        check_window(h, step0, n, "get_forcing");
+        const double* src = h->d_forcing.p + (size_t(var) * h->TW + (step0 - h->w0)) * h->n;
+        copy_rows(h->stream, dst, src, n * h->n * sizeof(double), dst_on_device, 1);
+    });
+}
+
+int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n) {
+    if (!h) return fail(h, "shyft_hip_synthetic_forcing: null handle");
+    return guarded(h, [&] {
+        check_window(h, step0, n, "synthetic_forcing");
+        update_derived(h);  // altitude row of the cell constants
+        const double* z = h->d_cellc.p + size_t(PC_ALTITUDE) * h->n;
+        hip_check(launch_synthetic_forcing(h->d_forcing.p, h->TW, step0 - h->w0, n, h->n, seed, cell_offset, step0, z,
+                                           h->stream),
+                  "synthetic_forcing");
+        hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_synthetic_elevation(uint64_t seed, uint64_t cell_offset, size_t n_cells, double* z_host) {
+    if (!z_host) return fail(nullptr, "shyft_hip_synthetic_elevation: null argument");
+    for (size_t i = 0; i < n_cells; ++i) z_host[i] = synth_elevation(seed, cell_offset + i);
+    return 0;
+}
+
+static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
+    update_derived(h);
+    size_t b = n_steps > 0 ? size_t(start_step) : 0;
+    size_t e = n_steps > 0 ? size_t(start_step + n_steps) : h->T;
+    check_window(h, b, e - b, "run_cells");
+    ptgsk_kargs a;
+    a.n_cells = int(h->n);
+    a.step0 = int(b);
+    a.n_steps = int(e - b);
+    a.win0 = int(h->w0);
+    a.win_len = int(h->TW);
+    a.collect = h->collect;
+    a.dt_s = double(h->dt) / 1e6;
+    a.dt_us = double(h->dt);
+    a.t1_hours = a.dt_s / 3600.0;  // to_seconds(T1-T0)/to_seconds(deltahours(1))
+    a.doy = h->d_doy.p;
+    a.t_rel_year_us = h->d_trel.p;
+    a.params = h->d_params.p;
+    a.set_ix = h->d_set_ix.p;
+    a.cellc = h->d_cellc.p;
+    a.state = h->d_state.p;
+    a.forcing = h->d_forcing.p;
+    a.resp = h->d_resp.p;
+    a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
+    a.active = h->active.empty() ? nullptr : h->d_active.p;
+    a.err = h->d_err.p;
+    hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
+    hip_check(launch_ptgsk_run(a, h->stream), "ptgsk_run_kernel launch");
+    hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
+}
+
+static void finish_run(shyft_hip_region* h) {
+    hip_check(hipStreamSynchronize(h->stream), "ptgsk_run_kernel");
+    float ms = 0.f;
+    hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
+    h->last_ms = ms;
+    std::vector<int32_t> errs(h->n);
+    // cheap check: reduce on host only when the kernel flagged something
+    hip_check(hipMemcpy(errs.data(), h->d_err.p, h->n * sizeof(int32_t), hipMemcpyDeviceToHost), "download err");
+    for (size_t i = 0; i < h->n; ++i)
+        if (errs[i]) {
+            hip_check(hipMemset(h->d_err.p, 0, h->n * sizeof(int32_t)), "memset");
+            throw std::runtime_error("kirchner: Max number of iterations exceeded (500). A new step size was not found. (cell " +
+                                     std::to_string(i) + ")");
+        }
+}
+
+int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {
+    if (!h) return fail(h, "shyft_hip_run_cells: null handle");
+    return guarded(h, [&] {
+        // argument checks of region_model::run_cells (region_model.h:579-592)
+        const size_t ncore = 4096;  // the GPU path accepts any use_ncore the reference would
+        if (use_ncore > 100 * ncore)
+            throw std::runtime_error("illegal parameter value: use_ncore(" + std::to_string(use_ncore) +
+                                     " is more than 100 time available physical cores: " + std::to_string(ncore));
+        if (!(h->T > 0)) throw std::runtime_error("region_model::run with invalid time_axis invoked");
+        if (start_step < 0 || size_t(start_step + 1) > h->T)
+            throw std::runtime_error("region_model::run start_step must in range[0..n_steps-1>");
+        if (n_steps < 0) throw std::runtime_error("region_model::run n_steps must be range[0..time-axis-steps]");
+        if (size_t(start_step + n_steps) > h->T)
+            throw std::runtime_error("region_model::run start_step+n_steps must be within time-axis range");
+        if (!h->has_state) throw std::runtime_error("region_model::run: no state set");
+        launch_run(h, start_step, n_steps);
+        finish_run(h);
+    });
+}
+
+int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps) {
+    if (!h) return fail(h, "shyft_hip_run_cells_async: null handle");
+    return guarded(h, [&] { launch_run(h, start_step, n_steps); });
+}
+
+int shyft_hip_synchronize(shyft_hip_region* h) {
+    if (!h) return fail(h, "shyft_hip_synchronize: null handle");
+    return guarded(h, [&] { finish_run(h); });
+}
+
+double shyft_hip_last_run_ms(const shyft_hip_region* h) { return h ? h->last_ms : 0.0; }
+
+int shyft_hip_get_series(const shyft_hip_region* hc, int series, size_t step0, size_t n, double* dst, int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_get_series: null argument");
+    return guarded(h, [&] {
+        if (series < 0 || size_t(series) >= h->n_series())
+            throw std::runtime_error("get_series: series not collected in this collection mode");
+        check_window(h, step0, n, "get_series");
+        const double* src = h->d_resp.p + (size_t(series) * h->TW + (step0 - h->w0)) * h->n;
+        copy_rows(h->stream, dst, src, n * h->n * sizeof(double), dst_on_device, 1);
+    });
+}
+
+int shyft_hip_get_state_series(const shyft_hip_region* hc, int field, size_t step0, size_t n, double* dst,
+                               int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_get_state_series: null argument");
+    return guarded(h, [&] {
+        if (!h->collect_state) throw std::runtime_error("get_state_series: state collection is off");
+        if (field < 0 || field >= PTGSK_NS) throw std::runtime_error("get_state_series: invalid field");
+        if (step0 < h->w0 || step0 + n > h->w0 + h->TW + 1) throw std::runtime_error("get_state_series: outside window");
+        const double* src = h->d_state_series.p + (size_t(field) * (h->TW + 1) + (step0 - h->w0)) * h->n;
+        copy_rows(h->stream, dst, src, n * h->n * sizeof(double), dst_on_device, 1);
+    });
+}
+
+int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* ids, size_t n_ids, int scope, int weighted,
+                         size_t step0, size_t n, double* dst) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_statistics: null argument");
+    return guarded(h, [&] {
+        if (series < 0 || size_t(series) >= h->n_series())
+            throw std::runtime_error("statistics: series not collected in this collection mode");
+        check_window(h, step0, n, "statistics");
+        std::vector<int32_t> sel = select_cells(h, ids, n_ids, scope);
+        if (sel.empty()) {  // no match: sum -> empty ts in the reference; average -> nan
+            for (size_t t = 0; t < n; ++t) dst[t] = weighted ? NAN : 0.0;
+            return;
+        }
+        h->d_sel.alloc(std::max(h->d_sel.n, sel.size()));
+        hip_check(hipMemcpy(h->d_sel.p, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload sel");
+        double sum_area = 0.0;
+        const double* w = nullptr;
+        if (weighted) {
+            std::vector<double> a(sel.size());
+            for (size_t k = 0; k < sel.size(); ++k) {
+                a[k] = h->geo[size_t(sel[k]) * 11 + 3];
+                sum_area += a[k];
+            }
+            h->d_w.alloc(std::max(h->d_w.n, a.size()));
+            hip_check(hipMemcpy(h->d_w.p, a.data(), a.size() * sizeof(double), hipMemcpyHostToDevice), "upload w");
+            w = h->d_w.p;
+        }
+        h->d_tmp.alloc(std::max(h->d_tmp.n, n));
+        const double* src = h->d_resp.p + (size_t(series) * h->TW + (step0 - h->w0)) * h->n;
+        hip_check(launch_select_sum(src, h->n, n, h->d_sel.p, sel.size(), w, h->d_tmp.p, h->stream), "select_sum");
+        copy_rows(h->stream, dst, h->d_tmp.p, n * sizeof(double), 0, 1);
+        if (weighted) {
+            const double s = 1 / sum_area;  // scale_by(1/sum_area) (cell_model.h:252)
+            for (size_t t = 0; t < n; ++t) dst[t] *= s;
+        }
+    });
+}
+
+int shyft_hip_catchment_sums(const shyft_hip_region* hc, int series, size_t step0, size_t n, double* dst,
+                             int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_catchment_sums: null argument");
+    return guarded(h, [&] {
+        if (series < 0 || size_t(series) >= h->n_series())
+            throw std::runtime_error("catchment_sums: series not collected in this collection mode");
+        check_window(h, step0, n, "catchment_sums");
+        const size_t C = h->cix_to_cid.size();
+        const double* src = h->d_resp.p + (size_t(series) * h->TW + (step0 - h->w0)) * h->n;
+        double* out = dst;
+        if (!dst_on_device) {
+            h->d_tmp.alloc(std::max(h->d_tmp.n, C * n));
+            out = h->d_tmp.p;
+        }
+        hip_check(launch_segment_sums(src, h->n, n, h->d_seg_cells.p, h->d_seg_off.p, C, out, h->stream), "segment_sums");
+        if (!dst_on_device) copy_rows(h->stream, dst, out, C * n * sizeof(double), 0, 1);
+        else hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+size_t shyft_hip_number_of_catchments(const shyft_hip_region* h) { return h ? h->cix_to_cid.size() : 0; }
+
+int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids) {
+    if (!h || !cids) return fail(const_cast<shyft_hip_region*>(h), "shyft_hip_catchment_ids: null argument");
+    for (size_t c = 0; c < h->cix_to_cid.size(); ++c) cids[c] = h->cix_to_cid[c];
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+"""Thin Python owner of a C-ABI region handle (include/shyft_hip.h).
+
+This is plumbing for tests, the bench and the Python API layer: every call
+goes straight to libshyft_hip.so. Arrays are numpy (host) or, where a
+function takes `on_device`, a raw device pointer (e.g. torch tensor.data_ptr()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._native import check, lib
+
+PT_GS_K, HBV_STACK, PT_SS_K = 1, 2, 3
+TEMPERATURE, PRECIPITATION, WIND_SPEED, REL_HUM, RADIATION = range(5)
+FORCING_NAMES = ("temperature", "precipitation", "wind_speed", "rel_hum", "radiation")
+COLLECT_DISCHARGE, COLLECT_DISCHARGE_SNOW, COLLECT_ALL = 0, 1, 2
+PTGSK_SERIES = ("avg_discharge", "charge_m3s", "snow_sca", "snow_swe", "snow_outflow", "glacier_melt", "ae_output",
+                "pe_output")
+PTGSK_STATE = ("albedo", "lwc", "surface_heat", "alpha", "sdc_melt_mean", "acc_melt", "iso_pot_energy", "temp_swe",
+               "kirchner_q")
+SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
+STACK_NPARAM = {PT_GS_K: 31}
+STACK_NSTATE = {PT_GS_K: 9}
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class HipRegion:
+    def __init__(self, stack: int, n_cells: int, device: int = -1):
+        self._L = lib()
+        h = C.c_void_p()
+        check(self._L.shyft_hip_region_create(stack, n_cells, device, C.byref(h)), None)
+        self.h = h
+        self.stack = stack
+        self.n = n_cells
+        self.n_steps = 0
+        self.window = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.shyft_hip_region_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, status):
+        check(status, self.h)
+
+    def set_geo(self, geo11: np.ndarray, routing_id=None, routing_distance=None):
+        g = np.ascontiguousarray(geo11, dtype=np.float64).reshape(self.n, 11)
+        rid = None if routing_id is None else np.ascontiguousarray(routing_id, dtype=np.int64)
+        rd = None if routing_distance is None else np.ascontiguousarray(routing_distance, dtype=np.float64)
+        self._chk(self._L.shyft_hip_set_geo(self.h, _ptr(g), _ptr(rid), _ptr(rd)))
+
+    def set_parameters(self, params: np.ndarray, set_ix: np.ndarray | None = None):
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        if p.ndim == 1:
+            p = p.reshape(1, -1)
+        ix = None if set_ix is None else np.ascontiguousarray(set_ix, dtype=np.int32)
+        self._chk(self._L.shyft_hip_set_parameters(self.h, _ptr(p), p.shape[0], p.shape[1], _ptr(ix)))
+
+    def set_time_axis(self, t0_us: int, dt_us: int, n_steps: int, window_steps: int = 0):
+        self._chk(self._L.shyft_hip_set_time_axis(self.h, int(t0_us), int(dt_us), int(n_steps), int(window_steps)))
+        self.n_steps = n_steps
+        self.window = n_steps if window_steps in (0, None) or window_steps > n_steps else window_steps
+
+    def set_window(self, w0: int):
+        self._chk(self._L.shyft_hip_set_window(self.h, int(w0)))
+
+    def set_collection(self, collect: int, collect_state: bool = False):
+        self._chk(self._L.shyft_hip_set_collection(self.h, int(collect), int(bool(collect_state))))
+
+    def set_catchment_filter(self, cids):
+        c = np.ascontiguousarray(cids, dtype=np.int64)
+        self._chk(self._L.shyft_hip_set_catchment_filter(self.h, _ptr(c) if c.size else None, c.size))
+
+    def set_state(self, state: np.ndarray):
+        s = np.ascontiguousarray(state, dtype=np.float64).reshape(self.n, -1)
+        self._chk(self._L.shyft_hip_set_state(self.h, _ptr(s), s.shape[1]))
+
+    def get_state(self, n_fields: int | None = None) -> np.ndarray:
+        nf = n_fields or STACK_NSTATE[self.stack]
+        s = np.empty((self.n, nf), dtype=np.float64)
+        self._chk(self._L.shyft_hip_get_state(self.h, _ptr(s), nf))
+        return s
+
+    def set_forcing(self, var: int, step0: int, values: np.ndarray):
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self.n)
+        self._chk(self._L.shyft_hip_set_forcing(self.h, var, step0, v.shape[0], _ptr(v), 0))
+
+    def set_forcing_device(self, var: int, step0: int, n: int, dev_ptr: int):
+        self._chk(self._L.shyft_hip_set_forcing(self.h, var, step0, n, C.c_void_p(dev_ptr), 1))
+
+    def get_forcing(self, var: int, step0: int, n: int) -> np.ndarray:
+        out = np.empty((n, self.n), dtype=np.float64)
+        self._chk(self._L.shyft_hip_get_forcing(self.h, var, step0, n, _ptr(out), 0))
+        return out
+
+    def synthetic_forcing(self, seed: int, step0: int, n: int, cell_offset: int = 0):
+        self._chk(self._L.shyft_hip_synthetic_forcing(self.h, seed, cell_offset, step0, n))
+
+    def run_cells(self, use_ncore: int = 0, start_step: int = 0, n_steps: int = 0):
+        self._chk(self._L.shyft_hip_run_cells(self.h, int(use_ncore), int(start_step), int(n_steps)))
+
+    def run_cells_async(self, start_step: int, n_steps: int):
+        self._chk(self._L.shyft_hip_run_cells_async(self.h, int(start_step), int(n_steps)))
+
+    def synchronize(self):
+        self._chk(self._L.shyft_hip_synchronize(self.h))
+
+    def last_run_ms(self) -> float:
+        return float(self._L.shyft_hip_last_run_ms(self.h))
+
+    def get_series(self, series: int, step0: int, n: int) -> np.ndarray:
+        out = np.empty((n, self.n), dtype=np.float64)
+        self._chk(self._L.shyft_hip_get_series(self.h, series, step0, n, _ptr(out), 0))
+        return out
+
+    def get_state_series(self, field: int, step0: int, n: int) -> np.ndarray:
+        out = np.empty((n, self.n), dtype=np.float64)
+        self._chk(self._L.shyft_hip_get_state_series(self.h, field, step0, n, _ptr(out), 0))
+        return out
+
+    def statistics(self, series: int, ids=(), scope: int = SCOPE_CATCHMENT, weighted: bool = False, step0: int = 0,
+                   n: int | None = None) -> np.ndarray:
+        n = self.n_steps - step0 if n is None else n
+        i = np.ascontiguousarray(list(ids), dtype=np.int64)
+        out = np.empty(n, dtype=np.float64)
+        self._chk(self._L.shyft_hip_statistics(self.h, series, _ptr(i) if i.size else None, i.size, scope,
+                                               int(weighted), step0, n, _ptr(out)))
+        return out
+
+    def number_of_catchments(self) -> int:
+        return int(self._L.shyft_hip_number_of_catchments(self.h))
+
+    def catchment_ids(self) -> np.ndarray:
+        c = np.empty(self.number_of_catchments(), dtype=np.int64)
+        self._chk(self._L.shyft_hip_catchment_ids(self.h, _ptr(c)))
+        return c
+
+    def catchment_sums(self, series: int, step0: int, n: int) -> np.ndarray:
+        out = np.empty((self.number_of_catchments(), n), dtype=np.float64)
+        self._chk(self._L.shyft_hip_catchment_sums(self.h, series, step0, n, _ptr(out), 0))
+        return out
+
+    def catchment_sums_device(self, series: int, step0: int, n: int, dev_ptr: int):
+        self._chk(self._L.shyft_hip_catchment_sums(self.h, series, step0, n, C.c_void_p(dev_ptr), 1))

@@ -1,0 +1,114 @@
+"""Synthetic region + forcing, bit-identical to the device
+generator in shyft_amd/csrc/include_internal/synth_hash.h.
+
+Grid cells x = 500 + 1000*(i mod W), y = 500 + 1000*(i div W), W = ceil(sqrt(N)),
+z = 2000*u(seed, 7, i, 0), area 1e6 m2, fractions glacier 0.01 / lake 0.05 /
+reservoir 0.19 / forest 0.30 (test_region_model_stacks.py:25-26), slope 0.9,
+cid = 1 + i*C//N (contiguous catchment blocks). Time axis 2015-01-01Z hourly.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+SEED = 20251015
+T0_2015_US = 1420070400 * 1_000_000  # 2015-01-01T00:00:00Z
+HOUR_US = 3600 * 1_000_000
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _sm64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        z = x
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _key(seed: int, cell: np.ndarray, step: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        c = np.asarray(cell, dtype=np.uint64) * np.uint64(0xD1B54A32D192ED03)
+        return _sm64(_sm64(np.uint64(seed) ^ c) ^ np.asarray(step, dtype=np.uint64))
+
+
+def _u(key: np.ndarray, var: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        v = np.uint64(var) * np.uint64(0xA24BAED4963EE407)
+    return (_sm64(key ^ v) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+
+
+def elevation(n_cells: int, seed: int = SEED, cell_offset: int = 0) -> np.ndarray:
+    cells = np.arange(cell_offset, cell_offset + n_cells, dtype=np.uint64)
+    return 2000.0 * _u(_key(seed, cells, np.zeros_like(cells)), 7)
+
+
+def geo11(n_cells: int, n_catchments: int = 100, seed: int = SEED, cell_offset: int = 0,
+          n_total: int | None = None) -> np.ndarray:
+    """n_cells x 11 geo_cell_data_io rows of cells [cell_offset, cell_offset+n_cells) of an n_total-cell region."""
+    n_total = n_total or (cell_offset + n_cells)
+    i = np.arange(cell_offset, cell_offset + n_cells, dtype=np.int64)
+    W = int(math.ceil(math.sqrt(n_total)))
+    g = np.zeros((n_cells, 11), dtype=np.float64)
+    g[:, 0] = 500.0 + 1000.0 * (i % W)
+    g[:, 1] = 500.0 + 1000.0 * (i // W)
+    g[:, 2] = elevation(n_cells, seed, cell_offset)
+    g[:, 3] = 1.0e6
+    g[:, 4] = 1 + (i * n_catchments) // n_total
+    g[:, 5] = 0.9
+    g[:, 6:10] = (0.01, 0.05, 0.19, 0.30)
+    g[:, 10] = 1.0 - 0.01 - 0.05 - 0.19 - 0.30
+    return g
+
+
+def forcing(n_cells: int, step0: int, n_steps: int, seed: int = SEED, cell_offset: int = 0,
+            z: np.ndarray | None = None) -> np.ndarray:
+    """[5][n_steps][n_cells] temperature, precipitation, wind_speed, rel_hum, radiation."""
+    if z is None:
+        z = elevation(n_cells, seed, cell_offset)
+    cells = np.arange(cell_offset, cell_offset + n_cells, dtype=np.uint64)[None, :]
+    steps = np.arange(step0, step0 + n_steps, dtype=np.uint64)[:, None]
+    key = _key(seed, cells, steps)
+    f = (steps % np.uint64(8760)).astype(np.float64) / 8760.0
+    g = f * (1.0 - f)
+    b = 16.0 * g * g
+    h = (steps % np.uint64(24)).astype(np.float64)
+    dd = (h - 12.0) / 6.0
+    di = 1.0 - dd * dd
+    di = np.where(di < 0.0, 0.0, di)
+    u0, u1, u2, u3, u5 = (_u(key, k) for k in (0, 1, 2, 3, 5))
+    out = np.empty((5, n_steps, n_cells), dtype=np.float64)
+    out[0] = 8.0 + 12.0 * (2.0 * b - 1.0) - 0.006 * z[None, :] + 4.0 * (u0 - 0.5)
+    out[1] = np.where(u1 < 0.15, 3.0 * u5, 0.0)
+    out[2] = 10.0 * u2
+    out[3] = 0.5 + 0.5 * u3
+    out[4] = np.broadcast_to(800.0 * di * (0.3 + 0.7 * b), (n_steps, n_cells))
+    return out
+
+
+def default_ptgsk_parameters() -> np.ndarray:
+    """PTGSKParameter() defaults in the reference get/set order (core/pt_gs_k.h:77-112)."""
+    return np.array([
+        -2.439, 0.966, -0.10,            # kirchner c1 c2 c3 (kirchner.h:120-125)
+        1.5,                             # ae.ae_scale_factor
+        -0.5, 2.0, 0.1, 1.0,             # gs.tx wind_scale max_water wind_const (gamma_snow.h:46-65)
+        5.0, 5.0, 30.0, 0.9, 0.6, 5.0,   # fast/slow albedo decay, surface_magnitude, max/min albedo, snowfall_reset_depth
+        0.4, 0.4,                        # snow_cv, glacier_albedo
+        1.0,                             # p_corr.scale_factor
+        0.0, 0.0,                        # snow_cv_forest_factor, snow_cv_altitude_factor
+        0.2, 1.26,                       # pt.albedo pt.alpha
+        0.04, 100.0, 0.0,                # initial_bare_ground_fraction, winter_end_day_of_year, calculate_iso_pot_energy
+        6.0,                             # gm.dtf
+        1.0, 7.0, 0.0,                   # routing velocity alpha beta (routing.h:76)
+        221.0,                           # gs.n_winter_days
+        0.0,                             # gm.direct_response
+        1.0,                             # msp.reservoir_direct_response_fraction
+    ], dtype=np.float64)
+
+
+def default_ptgsk_state(n_cells: int, q: float = 1.0) -> np.ndarray:
+    """PTGSKState() defaults (gamma_snow.h:101-116) with kirchner.q = q."""
+    s = np.empty((n_cells, 9), dtype=np.float64)
+    s[:] = (0.4, 0.1, 30000.0, 1.26, 0.0, 0.0, 0.0, 0.0, q)
+    return s

@@ -1,0 +1,53 @@
+"""Run one small pt_gs_k region on either engine with the same call:
+'oracle' (CPU restatement, the checker) or 'hip' (the product C ABI on the GPU)."""
+from __future__ import annotations
+
+import numpy as np
+
+from tests import oracle_lib
+
+
+def geo_row(x=1000.0, y=1000.0, z=100.0, area=1.0e6, cid=-1, slope=0.9, glacier=0.0, lake=0.0, reservoir=0.0,
+            forest=0.0):
+    return np.array([x, y, z, area, cid, slope, glacier, lake, reservoir, forest,
+                     1.0 - glacier - lake - reservoir - forest], dtype=np.float64)
+
+
+def ltf(glacier, lake, reservoir, forest, unspecified):
+    """land_type_fractions(glacier, lake, reservoir, forest, unspecified) ctor normalisation (geo_cell_data.h:36-51)."""
+    v = np.maximum(0.0, np.array([glacier, lake, reservoir, forest, unspecified], dtype=np.float64))
+    s = v.sum()
+    return v[:4] / s if s > 0 else np.zeros(4)
+
+
+def run(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, full=True,
+        collect_state=False):
+    """forcing [5][T][N]; returns dict main [2][T][N], full [8][T][N], state [N][9] (+ state_series)."""
+    geo11 = np.atleast_2d(geo11)
+    if engine == "oracle":
+        return oracle_lib.ptgsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step, n_steps, set_ix, full=full,
+                                    collect_state=collect_state)
+    from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_ALL, COLLECT_DISCHARGE
+    N = geo11.shape[0]
+    T = forcing.shape[1]
+    r = HipRegion(PT_GS_K, N)
+    try:
+        r.set_geo(geo11)
+        r.set_parameters(np.atleast_2d(params), set_ix)
+        r.set_time_axis(t0_us, dt_us, T)
+        r.set_collection(COLLECT_ALL if full else COLLECT_DISCHARGE, collect_state)
+        r.set_state(np.asarray(state).reshape(N, 9))
+        for v in range(5):
+            r.set_forcing(v, 0, forcing[v])
+        r.run_cells(0, start_step, n_steps)
+        out = {"state": r.get_state()}
+        ns = 8 if full else 2
+        allser = np.stack([r.get_series(k, 0, T) for k in range(ns)])
+        out["main"] = allser[:2]
+        if full:
+            out["full"] = allser
+        if collect_state:
+            out["state_series"] = np.stack([r.get_state_series(k, 0, T + 1) for k in range(9)])
+        return out
+    finally:
+        r.close()

@@ -1,0 +1,98 @@
+"""ctypes loader for the CPU oracle (oracle/_build/liboracle.so).
+
+Test infrastructure only: used by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py as the checker / baseline, never by shyft_amd.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+_L = None
+_d = C.c_double
+_dp = C.POINTER(C.c_double)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+_CACHE = {}
+
+
+def load(variant: str = "detmath"):
+    """variant 'detmath' (bit-exact checker of the HIP kernels) or 'libm' (host libm, as the reference)."""
+    if variant in _CACHE:
+        return _CACHE[variant]
+    path = LIB if variant == "detmath" else os.path.join(ORACLE_DIR, "_build", "liboracle_libm.so")
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    for fn in ("oracle_exp", "oracle_log", "oracle_lgamma_fn"):
+        getattr(L, fn).restype = _d
+        getattr(L, fn).argtypes = [_d]
+    L.oracle_pow.restype = _d
+    L.oracle_pow.argtypes = [_d, _d]
+    L.oracle_gamma_p.restype = _d
+    L.oracle_gamma_p.argtypes = [_d, _d]
+    L.oracle_lgamma.restype = _d
+    L.oracle_lgamma.argtypes = [_d]
+    L.oracle_gs_calc_snow_state.argtypes = [_d] * 7 + [_dp, _dp]
+    L.oracle_gs_corr_lwc.restype = _d
+    L.oracle_gs_corr_lwc.argtypes = [_d] * 6
+    L.oracle_gs_step.restype = C.c_int
+    L.oracle_gs_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p] + [_d] * 7
+    L.oracle_kirchner_step.restype = C.c_int
+    L.oracle_kirchner_step.argtypes = [_d] * 5 + [C.c_int64, C.c_int64, _dp, _dp, _d, _d]
+    L.oracle_pt_pot_evap.restype = _d
+    L.oracle_pt_pot_evap.argtypes = [_d] * 5
+    L.oracle_day_of_year.restype = C.c_int
+    L.oracle_day_of_year.argtypes = [C.c_int64]
+    L.oracle_trim_year.restype = C.c_int64
+    L.oracle_trim_year.argtypes = [C.c_int64]
+    L.oracle_ptgsk_run.restype = C.c_int
+    L.oracle_ptgsk_run.argtypes = ([C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int64,
+                                    C.c_int64, C.c_size_t, C.c_int, C.c_int] + [C.c_void_p] * 8 +
+                                   [C.c_int, _dp, C.c_char_p, C.c_size_t])
+    _CACHE[variant] = L
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def ptgsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, full=False,
+              collect_state=False, ncore=0, variant="detmath"):
+    """Run the oracle region model. forcing: [5][T][N]. Returns dict with 'main' [2][T][N],
+    'full' [8][T][N] (if full), 'state_series' [9][T+1][N] (if collect_state), 'state' [N][9], 'elapsed_s'."""
+    L = load(variant)
+    geo11 = np.ascontiguousarray(geo11, dtype=np.float64)
+    N = geo11.shape[0]
+    params = np.ascontiguousarray(np.atleast_2d(params), dtype=np.float64)
+    st = np.ascontiguousarray(state, dtype=np.float64).reshape(N, 9).copy()
+    F = np.ascontiguousarray(forcing, dtype=np.float64)
+    T = F.shape[1]
+    ix = None if set_ix is None else np.ascontiguousarray(set_ix, dtype=np.int32)
+    out_main = np.empty((2, T, N))
+    out_full = np.empty((8, T, N)) if full else None
+    out_state = np.empty((9, T + 1, N)) if collect_state else None
+    el = C.c_double(0.0)
+    err = C.create_string_buffer(512)
+    rc = L.oracle_ptgsk_run(N, _p(geo11), _p(params), params.shape[0], _p(ix), _p(st), int(t0_us), int(dt_us), T,
+                            int(start_step), int(n_steps), _p(F[0]), _p(F[1]), _p(F[2]), _p(F[3]), _p(F[4]),
+                            _p(out_main), _p(out_full), _p(out_state), int(ncore), C.byref(el), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    r = {"main": out_main, "state": st, "elapsed_s": el.value}
+    if full:
+        r["full"] = out_full
+    if collect_state:
+        r["state_series"] = out_state
+    return r
