@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Headline benchmark: pt_gs_k region_model::run_cells cell-steps/s on MI355X.
+
+Workload (BASELINE.json configs[1]): pt_gs_k, 1M synthetic cells per GPU x 8760
+hourly steps, fp64. A bench "step" is one pass of the hot path over one batch:
+all cells of the rank advanced through one chunk of CHUNK=730 hourly steps
+(1/12 year) -- the chunk's forcing is generated into HBM by the device
+generator and run_cells runs the pt_gs_k kernel over it, state
+carried in HBM to the next chunk. --steps 12 therefore runs one full year.
+The per-cell fp64 forcing of a full year (350 GB at 1M cells) does not fit
+one GPU's 288 GB, hence the chunking; generating a chunk costs ~1% of the step
+and is inside the timed region (conservative).
+
+Multi-GPU (--gpus N, one process per GPU via torch.distributed.run): cells
+shard with no data-path collective (run_cells has no cross-cell coupling,
+region_model.h:972-1021), weak scaling: each rank owns 1M cells of an
+N x 1M-cell region. Timing: barrier + synchronize around exactly K steps,
+max over ranks.
+
+Extra fields: roofline (dominant kernel = ptgsk_run_kernel, HBM-bound
+accounting per SURVEY.md §8d, kernel time from HIP events on the region's
+stream) and cpu_baseline (the CPU oracle built with the host libm, run with the
+reference's scheduler -- use_ncore std::async workers pulling one cell per
+mutex-protected pos++, region_model.h:991-1021 -- on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "cell-steps/sec (cells×timesteps/wall) for pt_gs_k at 1/2/4/8 MI355X"
+CHUNK = 730
+YEAR = 8760
+HBM_PEAK_BPS = 8.0e12            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+READ_B_PER_CELL_STEP = 40        # T, P, WS, RH, RAD fp64
+WRITE_B_PER_CELL_STEP = 16       # avg_discharge, charge_m3s fp64
+STATE_B_PER_CELL_LAUNCH = 2 * 9 * 8  # state read + write once per launch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cells", type=int, default=1 << 20, help="cells per GPU (default 1,048,576)")
+    ap.add_argument("--chunk", type=int, default=CHUNK)
+    ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier_sync(pg, local):
+    import torch
+    if pg is not None:
+        pg.barrier()
+    torch.cuda.synchronize(local)
+
+
+def max_over_ranks(pg, local, v: float) -> float:
+    if pg is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local}")
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def build_region(cells, world, rank, local, chunk, n_steps_axis):
+    from shyft_amd import synthetic
+    from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_DISCHARGE
+    r = HipRegion(PT_GS_K, cells, device=local)
+    r.set_geo(synthetic.geo11(cells, n_catchments=100 * world, cell_offset=rank * cells, n_total=world * cells))
+    r.set_parameters(synthetic.default_ptgsk_parameters())
+    r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, n_steps_axis, chunk)
+    r.set_collection(COLLECT_DISCHARGE)
+    return r
+
+
+def run_year(r, cells, rank, chunk, k_steps, seed, state0):
+    """K bench steps from Jan 1: per chunk generate forcing into HBM, then run_cells."""
+    kernel_ms = []
+    r.set_state(state0)
+    for s in range(k_steps):
+        step0 = s * chunk
+        r.set_window(step0)
+        r.synthetic_forcing(seed, step0, chunk, cell_offset=rank * cells)
+        r.run_cells(0, step0, chunk)
+        kernel_ms.append(r.last_run_ms())
+    return kernel_ms
+
+
+def cpu_baseline(n_cells, threads):
+    """Reference-scheduler CPU run (oracle built with host libm) on n_cells x 8760."""
+    from shyft_amd import synthetic
+    from shyft_amd.region import HipRegion, PT_GS_K
+    from tests import oracle_lib
+    # forcing of the sample cells: identical bits from the device generator (tests/test_capi.py pins equality)
+    g = HipRegion(PT_GS_K, n_cells, device=0)
+    g.set_geo(synthetic.geo11(n_cells, n_total=1 << 20))
+    g.set_parameters(synthetic.default_ptgsk_parameters())
+    g.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, YEAR)
+    g.synthetic_forcing(synthetic.SEED, 0, YEAR)
+    f = np.stack([g.get_forcing(v, 0, YEAR) for v in range(5)])
+    g.close()
+    geo = synthetic.geo11(n_cells, n_total=1 << 20)
+    res = oracle_lib.ptgsk_run(geo, synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(n_cells),
+                               synthetic.T0_2015_US, synthetic.HOUR_US, f, ncore=threads, variant="libm")
+    el = res["elapsed_s"]
+    # single-core rate on a small slice
+    n1 = min(200, n_cells)
+    r1 = oracle_lib.ptgsk_run(geo[:n1], synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(n1),
+                              synthetic.T0_2015_US, synthetic.HOUR_US, np.ascontiguousarray(f[:, :, :n1]), ncore=1,
+                              variant="libm")
+    return {
+        "value": n_cells * YEAR / el,
+        "unit": "cell-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n_cells} cells x {YEAR} hourly steps of the same synthetic region (first cells of the 1M-cell "
+                  f"region), oracle restatement built with host libm, reference scheduler "
+                  f"(region_model.h:991-1021) with use_ncore={threads}; run_cells wall {el:.2f}s",
+        "single_core_value": n1 * YEAR / r1["elapsed_s"],
+        "cpu_model": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    a = parse()
+    world, rank, local, pg = dist_setup(a.gpus)
+    import torch  # noqa: F401  (device init / sync)
+    from shyft_amd import synthetic
+
+    cells, chunk = a.cells, a.chunk
+    n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
+    r = build_region(cells, world, rank, local, chunk, n_axis)
+    state0 = synthetic.default_ptgsk_state(cells)
+
+    # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
+    if a.warmup > 0:
+        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0)
+    barrier_sync(pg, local)
+    t0 = time.perf_counter()
+    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0)
+    barrier_sync(pg, local)
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(pg, local, wall)
+    avg_kernel_ms = max_over_ranks(pg, local, float(np.mean(kernel_ms)))
+
+    total_cell_steps = world * cells * chunk * a.steps
+    value = total_cell_steps / wall
+    bytes_per_launch = cells * chunk * (READ_B_PER_CELL_STEP + WRITE_B_PER_CELL_STEP) + cells * STATE_B_PER_CELL_LAUNCH
+    achieved = bytes_per_launch / (avg_kernel_ms * 1e-3)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "cell-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8d generator, seed 20251015; device-generated per chunk)",
+        "config": {
+            "workload": f"pt_gs_k region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
+                        f"({a.steps} chunks of {chunk}), discharge_collector, default PTGSKParameter",
+            "cells_per_gpu": cells,
+            "total_cells": world * cells,
+            "steps_per_chunk": chunk,
+            "parallelism": f"cells sharded over {world} GPU(s), no data-path collective",
+        },
+        "kernel_ms_per_step": avg_kernel_ms,
+        "kernel_cell_steps_per_s": world * cells * chunk / (avg_kernel_ms * 1e-3),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved / 1e9,
+            "peak": HBM_PEAK_BPS / 1e9,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_BPS,
+            "traffic": None,
+            "kernel": "ptgsk_run_kernel",
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "note": "56 B/cell-step (40 B forcing read + 16 B discharge/charge write) + 144 B/cell state per launch; "
+                    "the kernel is fp64-VALU bound, not HBM bound (DESIGN.md)",
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        out["cpu_baseline"] = cpu_baseline(a.cpu_cells, threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    r.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
