@@ -254,6 +254,112 @@ DM_FN double lgamma(double x) {
     return v - shift;
 }
 
+// ---------------------------------------------------------------- incomplete gamma
+// The method stacks call boost::math::gamma_p (gamma_snow.h:195-197). detmath
+// supplies it the way it supplies libm: one deterministic implementation used
+// by both the kernels and the oracle. M is the elementary-function policy
+// (detmath itself, or the host libm for the oracle's libm variant).
+//
+// gamma_pq(a, x, lga) returns P(a,x), P(a+1,x) and prefix = x^a e^-x / Gamma(a)
+// (lga = lgamma(a) supplied by the caller).
+//   x < a+1 : series P(a,x) = prefix * sum_{n>=0} x^n / (a(a+1)...(a+n)), summed as
+//             a rational (B + E) / (a E) with E = (a+1)...(a+n) and
+//             B = sum_{k>=1} x^k E/(a+1..a+k) — one division instead of one per term.
+//             P(a+1,x) = prefix * B / (a E) (the n>=1 tail; no cancellation).
+//   x >= a+1: continued fraction Q(a,x) = prefix / (b0 + a1/(b1 + a2/(b2 + ...))),
+//             b_i = x + 2i + 1 - a, a_i = -i (i - a), by the forward (Wallis)
+//             recurrence with rescaling; P = 1 - Q, P(a+1,x) = 1 - (Q + prefix/a).
+// Terms are added until the next one is below 2^-52 of the sum (at most 2000).
+struct gamma_pq_result {
+    double p, p1, prefix;
+};
+
+struct dm_policy {
+    DM_FN static double exp(double x) { return detmath::exp(x); }
+    DM_FN static double log(double x) { return detmath::log(x); }
+};
+
+template <class M>
+DM_FN gamma_pq_result gamma_pq(double a, double x, double lga, double eps = 2.220446049250313e-16) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    gamma_pq_result r;
+    if (is_nan(a) || is_nan(x)) {
+        r.p = r.p1 = r.prefix = qnan();
+        return r;
+    }
+    if (x <= 0.0) {
+        r.p = r.p1 = r.prefix = 0.0;
+        return r;
+    }
+    if (x == inf()) {
+        r.p = r.p1 = 1.0;
+        r.prefix = 0.0;
+        return r;
+    }
+    const double prefix = M::exp(a * M::log(x) - x - lga);
+    r.prefix = prefix;
+    const double SCALE_HI = 1.0e200, SCALE = 6.2230152778611417e-61;  // 2^-200
+    if (x < a + 1.0) {
+        double ap = a, E = 1.0, B = 0.0, xn = 1.0;
+        for (int n = 1; n <= 2000; ++n) {
+            ap = ap + 1.0;
+            xn = xn * x;
+            E = E * ap;
+            B = DM_FMA(B, ap, xn);
+            if (xn < eps * (B + E)) break;
+            if (E > SCALE_HI) {
+                E = E * SCALE;
+                B = B * SCALE;
+                xn = xn * SCALE;
+            }
+        }
+        const double aE = a * E;
+        const double p = prefix * ((B + E) / aE);
+        const double p1 = prefix * (B / aE);
+        r.p = p < 1.0 ? p : 1.0;
+        r.p1 = p1 < 1.0 ? p1 : 1.0;
+        return r;
+    }
+    // Wallis recurrence for K = b0 + a1/(b1 + a2/(b2 + ...)); Q = prefix / K
+    double b = x + 1.0 - a;
+    double Pm = 1.0, Qm = 0.0;  // n-1
+    double P = b, Qd = 1.0;     // n (= 0)
+    for (int i = 1; i <= 2000; ++i) {
+        const double an = -i * (i - a);
+        b = b + 2.0;
+        const double Pn = DM_FMA(b, P, an * Pm);
+        const double Qn = DM_FMA(b, Qd, an * Qm);
+        // |Pn/Qn - P/Qd| < eps |Pn/Qn|  <=>  |Pn Qd - P Qn| < eps |Pn Qd|
+        const double cross = Pn * Qd;
+        const double diff = cross - P * Qn;
+        Pm = P; Qm = Qd;
+        P = Pn; Qd = Qn;
+        if ((diff < 0 ? -diff : diff) <= eps * (cross < 0 ? -cross : cross)) break;
+        const double aP = P < 0 ? -P : P;
+        if (aP > SCALE_HI) {
+            P = P * SCALE; Qd = Qd * SCALE; Pm = Pm * SCALE; Qm = Qm * SCALE;
+        }
+    }
+    const double q = prefix * (Qd / P);
+    const double q1 = q + prefix / a;
+    const double p = 1.0 - q;
+    const double p1 = 1.0 - q1;
+    r.p = p > 0.0 ? p : 0.0;
+    r.p1 = p1 > 0.0 ? p1 : 0.0;
+    return r;
+}
+
+DM_FN double gamma_p(double a, double x) { return gamma_pq<dm_policy>(a, x, detmath::lgamma(a)).p; }
+
+// boost::math precision policies used by gamma_snow (gamma_snow.h:189-197):
+// gamma_p(a, .) with digits10<10> when a < 2, digits10<5> otherwise. boost maps
+// digits10<d> to digits2 = (d+1)*1000/301 bits and stops its series / continued
+// fractions at a relative term size of ldexp(1, 1 - digits2):
+//   digits10<10> -> 36 bits -> 2^-35;  digits10<5> -> 19 bits -> 2^-18.
+DM_FN double gamma_snow_policy_eps(double a) { return a < 2.0 ? 0x1p-35 : 0x1p-18; }
+
 }  // namespace detmath
 
 #endif  // SHYFT_DETMATH_H

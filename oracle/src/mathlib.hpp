@@ -5,8 +5,12 @@
 // oracle is a bit-exact checker for the GPU path. Built with -DORACLE_LIBM the
 // oracle uses the host libm instead, as the reference build does; tests compare
 // the two variants to bound the effect of the elementary-function library.
+// The incomplete gamma (boost::math::gamma_p in the reference) always comes
+// from detmath::gamma_pq, evaluated with this build's exp/log.
 #pragma once
 #include <cmath>
+
+#include "../../detmath/detmath.h"
 
 #ifdef ORACLE_LIBM
 #define OEXP(x) std::exp(x)
@@ -14,7 +18,6 @@
 #define OPOW(x, y) std::pow(x, y)
 #define OLGAMMA(x) std::lgamma(x)
 #else
-#include "../../detmath/detmath.h"
 #define OEXP(x) detmath::exp(x)
 #define OLOG(x) detmath::log(x)
 #define OPOW(x, y) detmath::pow((double)(x), (double)(y))

@@ -82,47 +82,23 @@ inline double step(double dtf, double t, double snow_covered_area_m2, double gla
 // ---------------------------------------------------------------- special functions
 // The reference calls boost 1.68 boost::math::gamma_p / lgamma with reduced
 // precision policies (gamma_snow.h:189-201: digits10<10> for a<2, digits10<5>
-// otherwise). boost is not in /root/reference; this restatement evaluates the
-// regularized lower incomplete gamma to full double precision with the classic
-// series (x < a+1) / Lentz continued fraction (x >= a+1) split, so it agrees
-// with the reference to the reference's own ~1e-5 relative precision. The
-// known-answer tests (gamma_snow_test.cpp:76-115) pin it.
+// otherwise). boost is not in /root/reference; the restatement takes the
+// incomplete gamma from detmath (detmath/detmath.h: full double precision
+// series / continued fraction, the same implementation the kernels use, with
+// this build's elementary functions), so it agrees with the reference to the
+// reference's own ~1e-5 relative precision. The known-answer tests
+// (gamma_snow_test.cpp:76-115) pin it; tests/test_detmath.py checks it against
+// scipy.special.gammainc.
 namespace special {
+struct math_policy {
+    static double exp(double x) { return OEXP(x); }
+    static double log(double x) { return OLOG(x); }
+};
 inline double lgamma_(double a) { return OLGAMMA(a); }
-
-inline double gamma_p(double a, double x) {
-    if (std::isnan(a) || std::isnan(x)) return nan;
-    if (x <= 0.0) return 0.0;
-    if (std::isinf(x)) return 1.0;
-    const double eps = 2.220446049250313e-16;
-    const double prefix_log = a * OLOG(x) - x - lgamma_(a);
-    if (x < a + 1.0) {
-        double ap = a, del = 1.0 / a, sum = del;
-        for (int n = 0; n < 1000; ++n) {
-            ap += 1.0;
-            del *= x / ap;
-            sum += del;
-            if (std::fabs(del) < std::fabs(sum) * eps) break;
-        }
-        return std::min(1.0, sum * OEXP(prefix_log));
-    }
-    // continued fraction for Q(a,x), modified Lentz
-    const double fpmin = 1e-300;
-    double b = x + 1.0 - a, c = 1.0 / fpmin, d = 1.0 / b, h = d;
-    for (int i = 1; i < 1000; ++i) {
-        const double an = -i * (i - a);
-        b += 2.0;
-        d = an * d + b;
-        if (std::fabs(d) < fpmin) d = fpmin;
-        c = b + an / c;
-        if (std::fabs(c) < fpmin) c = fpmin;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (std::fabs(del - 1.0) < eps) break;
-    }
-    return std::max(0.0, 1.0 - OEXP(prefix_log) * h);
+inline detmath::gamma_pq_result gamma_pq(double a, double x, double eps = 2.220446049250313e-16) {
+    return detmath::gamma_pq<math_policy>(a, x, lgamma_(a), eps);
 }
+inline double gamma_p(double a, double x) { return gamma_pq(a, x).p; }
 
 // boost::math::tools::brent_find_minima (boost 1.68, tools/minima.hpp), restated:
 // bracket [min,max], start at max, golden constant 0.3819660f (a float literal),
@@ -233,11 +209,17 @@ struct calculator {
     static constexpr double sigma = 5.670373e-8;
     const double BB0 = 0.98 * sigma * OPOW(273.15, 4);
 
-    double gamma_p(double a, double b) const { return special::gamma_p(a, b); }
+    // gamma_snow.h:195-197: digits10<10> policy for a < 2, digits10<5> otherwise
+    double gamma_p(double a, double b) const { return special::gamma_pq(a, b, detmath::gamma_snow_policy_eps(a)).p; }
     double lgamma(double a) const { return special::lgamma_(a); }
 
     // gamma_snow.h:209-212
-    double calc_q(double a, double b, double z) const { return a * b * gamma_p(a + 1.0, z / b) + z * (1.0 - gamma_p(a, z / b)); }
+    // gamma_p(a+1, z/b) and gamma_p(a, z/b) come from one evaluation (detmath::gamma_pq),
+    // at the stricter of the two policies (that of a)
+    double calc_q(double a, double b, double z) const {
+        const auto g = special::gamma_pq(a, z / b, detmath::gamma_snow_policy_eps(a));
+        return a * b * g.p1 + z * (1.0 - g.p);
+    }
 
     // gamma_snow.h:214-227 (Brent, 12 bits, 60 iterations, bracket [0, z1])
     double corr_lwc(double z1, double a1, double b1, double /*z2*/, double a2, double b2) const {

@@ -145,3 +145,10 @@ int oracle_ptgsk_run(size_t n_cells, const double* geo11, const double* params, 
 }
 
 }  // extern "C"
+
+extern "C" void oracle_gamma_pq(double a, double x, double* p, double* p1, double* prefix) {
+    const auto r = special::gamma_pq(a, x);
+    *p = r.p;
+    *p1 = r.p1;
+    *prefix = r.prefix;
+}

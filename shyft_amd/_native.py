@@ -12,7 +12,7 @@ import threading
 _LIB = None
 _LOCK = threading.Lock()
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libshyft_hip.so")
+LIB_PATH = os.environ.get("SHYFT_HIP_LIB") or os.path.join(_HERE, "lib", "libshyft_hip.so")
 
 _dp = C.POINTER(C.c_double)
 _i32p = C.POINTER(C.c_int32)

@@ -20,7 +20,7 @@ constexpr double GS_TOL = 1.0e-10;  // gamma_snow::tol (gamma_snow.h:44)
 
 // ------------------------------------------------------------------ priestley-taylor
 // returns potential evapotranspiration in mm/s (priestley_taylor.h:75-102)
-__device__ inline double pt_pot_evap(double albedo, double alpha, double temperature, double global_radiation,
+__device__ SHYFT_INL_PT double pt_pot_evap(double albedo, double alpha, double temperature, double global_radiation,
                                      double rhumidity) {
     const bool neg = temperature < 0;
     const double ck2 = neg ? 17.84362 : 17.08085;
@@ -53,7 +53,7 @@ struct lgamma_cache {
 };
 
 // gamma_snow.h:230-260
-__device__ inline void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
+__device__ SHYFT_INL_SNOW void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
                                        double max_water_frac, double temp_swe, double& swe, double& sca,
                                        lgamma_cache& lgc) {
     double y = 0.0, y1 = 0.0;
@@ -66,7 +66,7 @@ __device__ inline void calc_snow_state(double shape, double scale, double y0, do
         return;
     } else {
         const double x = lambda / scale;
-        const gamma_p_result g = gamma_p_prefix(shape, x, lgc.get(shape));
+        const gamma_p_result g = gs_gamma_pq(shape, x, lgc.get(shape));
         y = g.p;
         y1 = y - g.prefix / shape;
         swe = m * (1.0 - y1) - lambda * (1 - y);
@@ -77,7 +77,7 @@ __device__ inline void calc_snow_state(double shape, double scale, double y0, do
     else if (lwd > 0.0) {
         const double sat = lwd / max_water_frac;
         const double x = sat / scale;
-        const gamma_p_result g = gamma_p_prefix(shape, x, lgc.get(shape));
+        const gamma_p_result g = gs_gamma_pq(shape, x, lgc.get(shape));
         const double ssa = g.p;
         const double ssa1 = ssa - g.prefix / shape;
         const double liqwat = max_water_frac * (m * (ssa1 - y1) + sat * (1.0 - ssa) - lambda * (1.0 - y));
@@ -87,19 +87,22 @@ __device__ inline void calc_snow_state(double shape, double scale, double y0, do
     swe *= 1.0 - y0;
 }
 
-// calc_q (gamma_snow.h:209-212)
-__device__ inline double gs_calc_q(double a, double b, double z, double lga, double lga1) {
-    const double x = z / b;
-    return a * b * gamma_p_prefix(a + 1.0, x, lga1).p + z * (1.0 - gamma_p_prefix(a, x, lga).p);
+// calc_q (gamma_snow.h:209-212); gamma_p(a+1, z/b) and gamma_p(a, z/b) from one gamma_pq
+__device__ inline double gs_calc_q(double a, double b, double z, double lga) {
+    const gamma_p_result g = gs_gamma_pq(a, z / b, lga);
+    return a * b * g.p1 + z * (1.0 - g.p);
 }
 
 // corr_lwc (gamma_snow.h:214-227): boost brent_find_minima over [0, z1],
 // 12 bits, 60 iterations; golden constant is the float literal 0.3819660f.
-__device__ inline double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2) {
-    const double Q1 = gs_calc_q(a1, b1, z1, dlgamma(a1), dlgamma(a1 + 1.0));
-    const double lga2 = dlgamma(a2), lga21 = dlgamma(a2 + 1.0);
+__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2) {
+#ifdef SHYFT_ABLATE_BRENT
+    return z1 * 0.5;  // timing ablation only (wrong results)
+#endif
+    const double Q1 = gs_calc_q(a1, b1, z1, dlgamma(a1));
+    const double lga2 = dlgamma(a2);
     auto f = [&](double z) {
-        const double v = gs_calc_q(a2, b2, z, lga2, lga21) - Q1;
+        const double v = gs_calc_q(a2, b2, z, lga2) - Q1;
         return v * v;
     };
     double min = 0.0, max = z1;
@@ -161,13 +164,28 @@ struct gs_cell {
     double inv_cv2;   // 1.0/cv2
 };
 
-// gamma_snow::calculator::step (gamma_snow.h:291-493). P is the per-set
-// parameter row (layout.h). dt_s = to_seconds(dt); prec_scale = dt/HOUR and
-// out_scale = HOUR/dt as the reference computes them from microsecond counts.
-__device__ inline void gs_step(gs_state& s, double& r_sca, double& r_storage, double& r_outflow, bool start_melt,
-                               bool snow_season, double dt_s, double dt_us, const double* __restrict__ P,
-                               const gs_cell& cc, double T, double rad, double prec_mm_h, double wind_speed,
-                               double rel_hum, lgamma_cache& lgc) {
+// gamma_snow::calculator::step (gamma_snow.h:291-493), split at its only
+// expensive, rarely taken call -- corr_lwc's Brent minimisation
+// (gamma_snow.h:425-435) -- so a workgroup can hand the Brent jobs of its lanes
+// to as few wavefronts as possible (see the kernel). gs_front runs everything up
+// to that point and says whether a Brent job is needed; gs_back finishes the
+// step given the Brent result. gs_step = front + Brent + back.
+// P is the per-set parameter row (layout.h); dt_s = to_seconds(dt), dt_us the
+// microsecond count (prec = prec_mm_h*dt/HOUR, outflow*HOUR/dt as the reference
+// evaluates them).
+struct gs_mid {
+    bool done;  // the early "no snow" path was taken (gamma_snow.h:313-322)
+    bool need;  // corr_lwc job: z1, a1, b1, a2, b2
+    double z1, a1, b1, a2, b2;
+    double prec, snow, rain, albedo, lwc, surface_heat, alpha, temp_swe, sca, storage, sdc_melt_mean, acc_melt,
+        iso_pot_energy, potential_melt, start_storage, sdc_scale;
+};
+
+__device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
+                                      const double* __restrict__ P, const gs_cell& cc, double T, double rad,
+                                      double prec_mm_h, double wind_speed, double rel_hum, lgamma_cache& lgc) {
+    m.need = false;
+    m.done = false;
     double sdc_melt_mean = s.sdc_melt_mean;
     double acc_melt = s.acc_melt;
     double iso_pot_energy = s.iso_pot_energy;
@@ -176,23 +194,18 @@ __device__ inline void gs_step(gs_state& s, double& r_sca, double& r_storage, do
     double snow, rain;
     if (T < P[PK_TX]) { snow = prec; rain = 0.0; }
     else { snow = 0.0; rain = prec; }
-
+    m.prec = prec;
+    m.acc_melt = acc_melt;
     if (snow < GS_TOL && sdc_melt_mean < GS_TOL && acc_melt < 0.0) {
-        s.albedo = P[PK_MAX_ALBEDO];
-        s.surface_heat = 0.0;
-        s.iso_pot_energy = 0.0;
-        r_sca = 0.0;
-        r_storage = 0.0;
-        r_outflow = prec_mm_h;
-        s.acc_melt = acc_melt;  // unchanged value written back (reference keeps s.acc_melt)
+        m.done = true;
         return;
     }
     double albedo = s.albedo;
     double lwc = s.lwc;
     double surface_heat = s.surface_heat;
     double alpha = s.alpha;
-    double temp_swe = s.temp_swe;
-    double sca = 0.0, storage = 0.0, outflow = 0.0;
+    const double temp_swe = s.temp_swe;
+    double sca = 0.0, storage = 0.0;
     const double min_albedo = P[PK_MIN_ALBEDO];
     const double max_albedo = P[PK_MAX_ALBEDO];
     const double ibgf = P[PK_IBGF];
@@ -233,11 +246,11 @@ __device__ inline void gs_step(gs_state& s, double& r_sca, double& r_storage, do
     delta_sh += surface_heat;
     double energy = effect * dt_s;
     if (delta_sh > 0.0) energy -= delta_sh;
-    double potential_melt = smax(0.0, energy / 333660.0);
+    const double potential_melt = smax(0.0, energy / 333660.0);
 
     double sdc_scale = sdc_melt_mean / alpha;
     calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
-    const double start_storage_value = storage;
+    m.start_storage = storage;
 
     if (acc_melt < 0.0) {
         if (snow < GS_TOL) snow = 0.0;
@@ -249,14 +262,55 @@ __device__ inline void gs_step(gs_state& s, double& r_sca, double& r_storage, do
             sdc_melt_mean += sdc_snow;
             sdc_scale = sdc_melt_mean / alpha;
             if (lwc > 0.0 && sdc_snow > 0.01 * sdc_melt_mean) {
-                double z1 = lwc / max_water;
-                double z1_guess = z1 * (1.0 - sdc_snow / sdc_melt_mean);
-                if (z1_guess < GS_TOL) z1_guess = z1 * 0.5;
-                (void)z1_guess;  // the reference computes but never uses the guess (gamma_snow.h:221-225)
-                z1 = gs_corr_lwc(z1, alpha_prev, sdc_scale_prev > 0.0 ? sdc_scale_prev : sdc_scale, alpha, sdc_scale);
-                lwc = z1 * max_water;
-                calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
+                // z1_guess (gamma_snow.h:427-430) is computed by the reference but unused by corr_lwc
+                m.need = true;
+                m.z1 = lwc / max_water;
+                m.a1 = alpha_prev;
+                m.b1 = sdc_scale_prev > 0.0 ? sdc_scale_prev : sdc_scale;
+                m.a2 = alpha;
+                m.b2 = sdc_scale;
             }
+        }
+    }
+    m.snow = snow;
+    m.rain = rain;
+    m.albedo = albedo;
+    m.lwc = lwc;
+    m.surface_heat = surface_heat;
+    m.alpha = alpha;
+    m.temp_swe = temp_swe;
+    m.sca = sca;
+    m.storage = storage;
+    m.sdc_melt_mean = sdc_melt_mean;
+    m.iso_pot_energy = iso_pot_energy;
+    m.potential_melt = potential_melt;
+    m.sdc_scale = sdc_scale;
+}
+
+__device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, double& r_sca, double& r_storage,
+                                     double& r_outflow, bool snow_season, double dt_us, const double* __restrict__ P,
+                                     const gs_cell& cc, double prec_mm_h, lgamma_cache& lgc) {
+    if (m.done) {
+        s.albedo = P[PK_MAX_ALBEDO];
+        s.surface_heat = 0.0;
+        s.iso_pot_energy = 0.0;
+        s.acc_melt = m.acc_melt;  // == s.acc_melt: the early path only triggers when it was not reset
+        r_sca = 0.0;
+        r_storage = 0.0;
+        r_outflow = prec_mm_h;
+        return;
+    }
+    const double ibgf = P[PK_IBGF];
+    const double max_water = P[PK_MAX_WATER];
+    double snow = m.snow;
+    const double rain = m.rain;
+    double lwc = m.lwc, alpha = m.alpha, temp_swe = m.temp_swe, sca = m.sca, storage = m.storage;
+    double sdc_melt_mean = m.sdc_melt_mean, acc_melt = m.acc_melt, potential_melt = m.potential_melt;
+    double sdc_scale = m.sdc_scale;
+    if (acc_melt < 0.0) {
+        if (m.need) {
+            lwc = z * max_water;
+            calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
         }
         lwc += rain;
         if (sdc_melt_mean <= potential_melt) {
@@ -303,21 +357,23 @@ __device__ inline void gs_step(gs_state& s, double& r_sca, double& r_storage, do
         }
     }
     calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
-    outflow = prec + start_storage_value - storage;
+    double outflow = m.prec + m.start_storage - storage;
     if (outflow < 0.0) outflow = 0.0;
 
-    s.albedo = albedo;
+    s.albedo = m.albedo;
     s.lwc = lwc;
-    s.surface_heat = surface_heat;
+    s.surface_heat = m.surface_heat;
     s.alpha = alpha;
     s.sdc_melt_mean = sdc_melt_mean;
     s.acc_melt = acc_melt;
-    s.iso_pot_energy = iso_pot_energy;
+    s.iso_pot_energy = m.iso_pot_energy;
     s.temp_swe = temp_swe;
     r_sca = sca;
     r_storage = storage;
     r_outflow = (outflow * 3600000000.0) / dt_us;
 }
+
+__device__ inline double gs_solve_lwc(const gs_mid& m) { return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2); }
 
 // ------------------------------------------------------------------ kirchner
 // kirchner.h:186-198
@@ -331,7 +387,7 @@ __device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, do
 // accepted) is flattened into one loop of try_steps so lanes of a wave that
 // need different numbers of attempts stay in one convergent loop.
 // Returns false if a do_step needed 500 attempts (odeint failed_step_checker).
-__device__ inline bool kirchner_step(double& q, double& q_avg, double p, double e, double t1, double c1, double c2,
+__device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, double e, double t1, double c1, double c2,
                                      double c3) {
     const double abs_err = 1.0e-7, rel_err = 1.0e-8;
     if (q < 0.00001) q = 0.00001;

@@ -21,56 +21,57 @@ namespace shyft_dev {
 
 __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
-__device__ __forceinline__ double dexp(double x) { return detmath::exp(x); }
-__device__ __forceinline__ double dlog(double x) { return detmath::log(x); }
-__device__ __forceinline__ double dpow(double x, double y) { return detmath::pow(x, y); }
-__device__ __forceinline__ double dlgamma(double x) { return detmath::lgamma(x); }
+// inlining policy of the heavy device functions (tuned for VGPR pressure / I-cache)
+#ifndef SHYFT_INL_SNOW
+#define SHYFT_INL_SNOW __noinline__
+#endif
+#ifndef SHYFT_INL_GS
+#define SHYFT_INL_GS inline
+#endif
+#ifndef SHYFT_INL_K
+#define SHYFT_INL_K inline
+#endif
+#ifndef SHYFT_INL_PT
+#define SHYFT_INL_PT inline
+#endif
+#ifndef SHYFT_INL_GP
+#define SHYFT_INL_GP inline
+#endif
+#ifndef SHYFT_DM_INLINE
+#define SHYFT_DM_INLINE __noinline__
+#endif
+#ifndef SHYFT_DM_INLINE_POW
+#define SHYFT_DM_INLINE_POW __noinline__
+#endif
+__device__ SHYFT_DM_INLINE double dexp(double x) { return detmath::exp(x); }
+__device__ SHYFT_DM_INLINE double dlog(double x) { return detmath::log(x); }
+__device__ SHYFT_DM_INLINE_POW double dpow(double x, double y) { return detmath::pow(x, y); }
+__device__ __noinline__ double dlgamma(double x) { return detmath::lgamma(x); }
 
-struct gamma_p_result {
-    double p;       // P(a, x)
-    double prefix;  // exp(a*log(x) - x - lgamma(a)); 0 when x <= 0
+// boost::math::gamma_p stand-in: detmath::gamma_pq (P(a,x), P(a+1,x) and the
+// prefix x^a e^-x / Gamma(a) from ONE series / continued-fraction evaluation),
+// with the out-of-line elementary functions above.
+struct dev_math {
+    __device__ static double exp(double x) { return dexp(x); }
+    __device__ static double log(double x) { return dlog(x); }
 };
+using gamma_p_result = detmath::gamma_pq_result;
 
-// lga = lgamma(a) supplied by the caller (shape changes rarely, so callers cache it)
-__device__ inline gamma_p_result gamma_p_prefix(double a, double x, double lga) {
-    gamma_p_result r;
-    if (x <= 0.0) { r.p = 0.0; r.prefix = 0.0; return r; }
-    if (__builtin_isinf(x)) { r.p = 1.0; r.prefix = 0.0; return r; }
-    const double eps = 2.220446049250313e-16;
-    const double prefix = dexp(a * dlog(x) - x - lga);
-    r.prefix = prefix;
-    if (x < a + 1.0) {
-        double ap = a, del = 1.0 / a, sum = del;
-        for (int n = 0; n < 1000; ++n) {
-            ap += 1.0;
-            del *= x / ap;
-            sum += del;
-            if (fabs(del) < fabs(sum) * eps) break;
-        }
-        r.p = smin(1.0, sum * prefix);
-        return r;
-    }
-    const double fpmin = 1e-300;
-    double b = x + 1.0 - a, c = 1.0 / fpmin, d = 1.0 / b, h = d;
-    for (int i = 1; i < 1000; ++i) {
-        const double an = -i * (i - a);
-        b += 2.0;
-        d = an * d + b;
-        if (fabs(d) < fpmin) d = fpmin;
-        c = b + an / c;
-        if (fabs(c) < fpmin) c = fpmin;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (fabs(del - 1.0) < eps) break;
-    }
-    r.p = smax(0.0, 1.0 - prefix * h);
-    return r;
+// lga = lgamma(a) supplied by the caller (shape changes rarely, so callers cache it);
+// eps = the relative termination tolerance (boost precision policy of the caller)
+__device__ SHYFT_INL_GP gamma_p_result gamma_p_prefix(double a, double x, double lga, double eps) {
+#ifdef SHYFT_ABLATE_GAMMA
+    gamma_p_result r; r.p = 0.5; r.p1 = 0.4; r.prefix = 0.01; return r;  // timing ablation only (wrong results)
+#endif
+    return detmath::gamma_pq<dev_math>(a, x, lga, eps);
 }
 
-__device__ inline double gamma_p(double a, double x) {
-    if (__builtin_isnan(a) || __builtin_isnan(x)) return __builtin_nan("");
-    return gamma_p_prefix(a, x, dlgamma(a)).p;
+// gamma_snow's calls: boost precision policy by shape (gamma_snow.h:195-197)
+__device__ inline gamma_p_result gs_gamma_pq(double a, double x, double lga) {
+    return gamma_p_prefix(a, x, lga, detmath::gamma_snow_policy_eps(a));
 }
+
+// full double precision (boost default policy)
+__device__ inline double gamma_p(double a, double x) { return gamma_p_prefix(a, x, dlgamma(a), 2.220446049250313e-16).p; }
 
 }  // namespace shyft_dev

@@ -6,6 +6,14 @@
 // with the cell state held in registers, forcing read [step][cell] (coalesced,
 // 512 B per wave per variable per step) and collector series written
 // [series][step][cell].
+//
+// Brent compaction (COMPACT = true): gamma_snow's corr_lwc Brent minimisation
+// (gamma_snow.h:425-435) costs ~30 incomplete-gamma evaluations and fires for a
+// random ~10% of cells on a snowfall step, so nearly every wavefront would run
+// it for a few lanes. Each step the workgroup queues its lanes' Brent jobs in LDS
+// and the first ceil(jobs/64) wavefronts solve them (one job per lane), then
+// every lane picks up its own result. Results are bit-identical to the
+// per-lane version: the same function on the same arguments.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -18,28 +26,39 @@ namespace {
 
 // error codes written to err[cell]
 constexpr int32_t ERR_KIRCHNER_MAX_ITER = 1;
+#ifndef SHYFT_BLOCK
+#define SHYFT_BLOCK 256
+#endif
+constexpr int BLOCK = SHYFT_BLOCK;
 
-__global__ __launch_bounds__(256) void ptgsk_run_kernel(const ptgsk_kargs a) {
+#ifndef SHYFT_LB_WAVES
+#define SHYFT_LB_WAVES 4
+#endif
+
+template <bool COMPACT>
+__global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= a.n_cells) return;
-    if (a.active && !a.active[cell]) return;
+    bool valid = cell < a.n_cells;
+    if (valid && a.active && !a.active[cell]) valid = false;
+    if (!COMPACT && !valid) return;
+    const int lc = valid ? cell : 0;  // out-of-range lanes of a COMPACT block read cell 0 and store nothing
     const size_t N = (size_t)a.n_cells;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * PTGSK_NP;
+    const double* __restrict__ P = a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
 
     // per-cell constants (pt_gs_k.h:347-357)
     const double* __restrict__ cc = a.cellc;
     gs_cell gcell;
-    gcell.forest_fraction = cc[PC_FOREST * N + cell];
-    gcell.altitude = cc[PC_ALTITUDE * N + cell];
-    gcell.cv2 = cc[PC_CV2 * N + cell];
-    gcell.inv_cv2 = cc[PC_INV_CV2 * N + cell];
-    const double glacier_fraction = cc[PC_GLACIER * N + cell];
-    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + cell];
-    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + cell];
-    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + cell];
-    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + cell];
-    const double cell_area_m2 = cc[PC_AREA * N + cell];
-    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + cell];
+    gcell.forest_fraction = cc[PC_FOREST * N + lc];
+    gcell.altitude = cc[PC_ALTITUDE * N + lc];
+    gcell.cv2 = cc[PC_CV2 * N + lc];
+    gcell.inv_cv2 = cc[PC_INV_CV2 * N + lc];
+    const double glacier_fraction = cc[PC_GLACIER * N + lc];
+    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
+    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
+    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + lc];
+    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + lc];
+    const double cell_area_m2 = cc[PC_AREA * N + lc];
+    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
 
     const double gm_direct = P[PK_GM_DIRECT];
     const double gm_routed = 1 - gm_direct;
@@ -51,15 +70,15 @@ __global__ __launch_bounds__(256) void ptgsk_run_kernel(const ptgsk_kargs a) {
     // state -> registers
     double* __restrict__ st = a.state;
     gs_state s;
-    s.albedo = st[PS_ALBEDO * N + cell];
-    s.lwc = st[PS_LWC * N + cell];
-    s.surface_heat = st[PS_SURFACE_HEAT * N + cell];
-    s.alpha = st[PS_ALPHA * N + cell];
-    s.sdc_melt_mean = st[PS_SDC_MELT_MEAN * N + cell];
-    s.acc_melt = st[PS_ACC_MELT * N + cell];
-    s.iso_pot_energy = st[PS_ISO_POT_ENERGY * N + cell];
-    s.temp_swe = st[PS_TEMP_SWE * N + cell];
-    double q = st[PS_KIRCHNER_Q * N + cell];
+    s.albedo = st[PS_ALBEDO * N + lc];
+    s.lwc = st[PS_LWC * N + lc];
+    s.surface_heat = st[PS_SURFACE_HEAT * N + lc];
+    s.alpha = st[PS_ALPHA * N + lc];
+    s.sdc_melt_mean = st[PS_SDC_MELT_MEAN * N + lc];
+    s.acc_melt = st[PS_ACC_MELT * N + lc];
+    s.iso_pot_energy = st[PS_ISO_POT_ENERGY * N + lc];
+    s.temp_swe = st[PS_TEMP_SWE * N + lc];
+    double q = st[PS_KIRCHNER_Q * N + lc];
     lgamma_cache lgc;
     int32_t err = 0;
 
@@ -77,6 +96,14 @@ __global__ __launch_bounds__(256) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int64_t snow_lo = (int64_t)((int)(P[PK_WED] * 24) - (int)(P[PK_NWD] * 24)) * 3600000000LL;
     const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
 
+    // Brent job queue of the workgroup (COMPACT)
+    __shared__ double jz1[BLOCK], ja1[BLOCK], jb1[BLOCK], ja2[BLOCK], jb2[BLOCK], jres[BLOCK];
+    __shared__ int jcount[2];
+    if (COMPACT) {
+        if (threadIdx.x == 0) jcount[0] = 0;
+        __syncthreads();
+    }
+
     auto collect_state = [&](size_t wi) {
         // state_collector::collect of state.scale_snow(snow_storage_fraction)
         SS[0 * SSS + wi * N + cell] = cell_area_m2 * q * mmh_to_m3s_scale_factor;
@@ -93,20 +120,53 @@ __global__ __launch_bounds__(256) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int i_end = a.step0 + a.n_steps;
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
-        const size_t fo = wi * N + cell;
-        const double temp = f_temp[fo];
-        const double rad = f_rad[fo];
-        const double rel_hum = f_rh[fo];
-        const double prec = f_prec[fo] * p_corr;
-        const double wind_speed = f_ws[fo];
-        if (SS) collect_state(wi);
-
+        const size_t fo = wi * N + lc;
+        double temp = 0, rad = 0, rel_hum = 0, prec = 0, wind_speed = 0;
+        if (valid) {
+            temp = f_temp[fo];
+            rad = f_rad[fo];
+            rel_hum = f_rh[fo];
+            prec = f_prec[fo] * p_corr;
+            wind_speed = f_ws[fo];
+            if (SS) collect_state(wi);
+        }
         const bool start_melt = a.doy[i] == wed;
         const int64_t trel = a.t_rel_year_us[i];
         const bool snow_season = trel >= snow_lo && trel < snow_hi;
+
+        gs_mid m;
+        m.need = false;
+        m.done = true;
+        if (valid)
+            gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc);
+        double z = 0.0;
+        if (COMPACT) {
+            if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (race-free: see DESIGN.md)
+            int slot = -1;
+            if (m.need) {
+                slot = atomicAdd(&jcount[i & 1], 1);
+                jz1[slot] = m.z1; ja1[slot] = m.a1; jb1[slot] = m.b1; ja2[slot] = m.a2; jb2[slot] = m.b2;
+            }
+            __syncthreads();
+            const int nj = jcount[i & 1];
+            if (nj > 0) {
+#ifdef SHYFT_ROTATE
+                // rotate which wavefront starts the queue so the Brent load spreads over the SIMDs
+                const int t = (threadIdx.x + BLOCK - 64 * (i % (BLOCK / 64))) % BLOCK;
+#else
+                const int t = threadIdx.x;
+#endif
+                for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j]);
+                __syncthreads();
+                if (slot >= 0) z = jres[slot];
+            }
+        } else if (m.need) {
+            z = gs_solve_lwc(m);
+        }
+        if (!valid) continue;
         double gs_sca, gs_storage, gs_outflow;
-        gs_step(s, gs_sca, gs_storage, gs_outflow, start_melt, snow_season, a.dt_s, a.dt_us, P, gcell, temp, rad, prec,
-                wind_speed, rel_hum, lgc);
+        gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc);
+
         // glacier_melt::step (glacier_melt.h:47-52)
         const double sca_area = cell_area_m2 * gs_sca;
         double gm_melt_m3s = 0.0;
@@ -139,6 +199,7 @@ __global__ __launch_bounds__(256) void ptgsk_run_kernel(const ptgsk_kargs a) {
         }
         if (SS && i + 1 == i_end) collect_state(wi + 1);
     }
+    if (!valid) return;
     st[PS_ALBEDO * N + cell] = s.albedo;
     st[PS_LWC * N + cell] = s.lwc;
     st[PS_SURFACE_HEAT * N + cell] = s.surface_heat;
@@ -153,10 +214,16 @@ __global__ __launch_bounds__(256) void ptgsk_run_kernel(const ptgsk_kargs a) {
 
 }  // namespace
 
+#ifndef SHYFT_COMPACT_DEFAULT
+#define SHYFT_COMPACT_DEFAULT 1
+#endif
+
 hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream) {
-    const int block = 256;
-    const int grid = (a.n_cells + block - 1) / block;
+    const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptgsk_run_kernel, dim3(grid), dim3(block), 0, stream, a);
+    if (SHYFT_COMPACT_DEFAULT)
+        hipLaunchKernelGGL(ptgsk_run_kernel<true>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    else
+        hipLaunchKernelGGL(ptgsk_run_kernel<false>, dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

@@ -61,3 +61,22 @@ def test_lgamma_against_scipy(libs):
     a = _vec(dm.oracle_lgamma_fn, x)
     b = sp.gammaln(x)
     assert (np.abs(a - b) / np.maximum(np.abs(b), 1.0)).max() < 5e-15
+
+
+def test_gamma_pq_against_scipy(libs):
+    import ctypes as C
+    sp = pytest.importorskip("scipy.special")
+    dm, _ = libs
+    rng = np.random.default_rng(11)
+    a = np.exp(rng.uniform(np.log(0.05), np.log(300.0), 6000))
+    x = a * rng.uniform(0.0, 3.0, a.size)
+    x[:50] = a[:50] + 1.0  # branch boundary
+    p, p1, pre = C.c_double(), C.c_double(), C.c_double()
+    worst = 0.0
+    for ai, xi in zip(a, x):
+        dm.oracle_gamma_pq(ai, xi, C.byref(p), C.byref(p1), C.byref(pre))
+        for got, want in ((p.value, sp.gammainc(ai, xi)), (p1.value, sp.gammainc(ai + 1, xi))):
+            err = abs(got - want) / max(abs(want), 1e-300)
+            # relative 1e-12, or absolute 1e-14 where P is tiny / its complement dominates
+            worst = max(worst, min(err, abs(got - want) / 1e-2))
+            assert err < 1e-12 or abs(got - want) < 1e-14, (ai, xi, got, want)
