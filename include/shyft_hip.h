@@ -100,6 +100,23 @@ int shyft_hip_get_state(const shyft_hip_region* h, double* state, size_t n_field
 int shyft_hip_set_forcing(shyft_hip_region* h, int var, size_t step0, size_t n, const double* src, int src_on_device);
 int shyft_hip_get_forcing(const shyft_hip_region* h, int var, size_t step0, size_t n, double* dst, int dst_on_device);
 
+/* Inverse-distance interpolation of one forcing variable from n_sources geo-located sources
+ * into the cells (region_model::interpolate's per-variable idw::run_interpolation,
+ * core/region_model.h:456-515, core/inverse_distance.h:142-250), for steps [step0, step0+n)
+ * of the resident window. Only cells passing the catchment calculation filter are written.
+ *  src_xyz    : n_sources x 3 (geo_point x y z)
+ *  src_values : [n][n_sources], the sources already averaged onto the model time axis
+ *               (the average_accessor step, region_model.h:135-145, is the caller's)
+ *  idw_param  : max_members (<= 32), max_distance, distance_measure_factor, zscale,
+ *               default_temp_gradient, gradient_by_equation (0/1), precipitation scale_factor
+ *               (inverse_distance.h:38-74)
+ * Model by variable: temperature (gradient transform), precipitation (scale^(dz/100)),
+ * radiation (x slope factor), wind_speed and rel_hum (plain). A single temperature source is
+ * copied to every cell as the reference does (region_model.h:470-481). The neighbour table is
+ * built on the first call and reused while sources and parameters are unchanged. */
+int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const double* src_xyz,
+                          const double* src_values, size_t step0, size_t n, const double* idw_param);
+
 /* Deterministic synthetic forcing for steps [step0, step0+n) of the resident window,
  * generated on device (bench/test workload; SURVEY.md §8d generator). */
 int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n);

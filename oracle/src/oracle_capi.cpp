@@ -7,6 +7,7 @@
 #include <exception>
 
 #include "common.hpp"
+#include "idw.hpp"
 #include "methods.hpp"
 #include "ptgsk.hpp"
 #include "region.hpp"
@@ -145,6 +146,44 @@ int oracle_ptgsk_run(size_t n_cells, const double* geo11, const double* params, 
 }
 
 }  // extern "C"
+
+// Inverse-distance interpolation of one variable (kind: 0 temperature, 1 precipitation,
+// 2 radiation, 3 wind_speed, 4 rel_hum). src_values [T][S], out [T][N].
+// param: max_members, max_distance, distance_measure_factor, zscale, default_temp_gradient,
+//        gradient_by_equation, precipitation scale_factor
+extern "C" int oracle_idw_run(int kind, size_t S, const double* src_xyz, const double* src_values, size_t N,
+                              const double* dst_xyz, const double* dst_slope, size_t T, const double* param, double* out) {
+    idw::parameter p;
+    p.max_members = size_t(param[0]);
+    p.max_distance = param[1];
+    p.distance_measure_factor = param[2];
+    p.zscale = param[3];
+    p.default_temp_gradient = param[4];
+    p.gradient_by_equation = param[5] != 0.0;
+    p.scale_factor = param[6];
+    std::vector<std::vector<double>> vals(S, std::vector<double>(T));
+    std::vector<idw::source> src(S);
+    for (size_t s = 0; s < S; ++s) {
+        for (size_t t = 0; t < T; ++t) vals[s][t] = src_values[t * S + s];
+        src[s] = idw::source{geo_point(src_xyz[3 * s], src_xyz[3 * s + 1], src_xyz[3 * s + 2]), vals[s].data()};
+    }
+    std::vector<idw::destination> dst(N);
+    for (size_t j = 0; j < N; ++j)
+        dst[j] = idw::destination{geo_point(dst_xyz[3 * j], dst_xyz[3 * j + 1], dst_xyz[3 * j + 2]), dst_slope ? dst_slope[j] : 0.9};
+    idw::run(idw::model_kind(kind), src, dst, T, p, out);
+    return 0;
+}
+
+extern "C" double oracle_idw_temperature_gradient(size_t n, const double* xyz, const double* t, double default_gradient,
+                                                  int by_equation) {
+    std::vector<geo_point> pts;
+    std::vector<double> tv;
+    for (size_t i = 0; i < n; ++i) {
+        pts.emplace_back(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+        tv.push_back(t[i]);
+    }
+    return idw::temperature_gradient(pts, tv, default_gradient, by_equation != 0);
+}
 
 extern "C" void oracle_gamma_pq(double a, double x, double* p, double* p1, double* prefix) {
     const auto r = special::gamma_pq(a, x);

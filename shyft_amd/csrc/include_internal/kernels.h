@@ -46,3 +46,37 @@ hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_st
 
 // fill with a constant
 hipError_t launch_fill(double* p, size_t n, double v, hipStream_t stream);
+
+// inverse-distance interpolation (kernels/idw.hip)
+#define IDW_KMAX 32
+enum idw_kind { IDW_TEMPERATURE = 0, IDW_PRECIPITATION = 1, IDW_RADIATION = 2, IDW_WIND_SPEED = 3, IDW_REL_HUM = 4 };
+
+struct idw_nb_args {
+    int n_cells, n_sources, kind, max_members;
+    double max_distance, distance_measure_factor, zscale, scale_factor;
+    const double* src_xyz;  // [S][3]
+    const double* dst_xyz;  // [N][3]
+    int32_t* idx;           // [K][N] source index, -1 beyond count
+    double* w;              // [K][N] weight
+    double* aux;            // [K][N] temperature: d.z - s.z; precipitation: pow(scale, (d.z - s.z)/100)
+    int32_t* count;         // [N]
+};
+
+struct idw_gather_args {
+    int n_cells, n_sources, n_rows, kind, by_equation;
+    double default_gradient;
+    const double* src_xyz;     // [S][3]
+    const double* src_values;  // [n_rows][S]
+    const double* slope;       // [N] radiation slope factor (geo_cell_data)
+    const int32_t* idx;
+    const double* w;
+    const double* aux;
+    const int32_t* count;
+    const uint8_t* active;     // catchment calculation filter or null
+    double* out;               // [n_rows][N] (a forcing window slice)
+};
+
+hipError_t launch_idw_neighbours(const idw_nb_args& a, hipStream_t stream);
+hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream);
+hipError_t launch_copy_source(const double* v, int n_rows, int n_cells, const uint8_t* active, double* out,
+                              hipStream_t stream);

@@ -121,6 +121,17 @@ struct shyft_hip_region {
     dbuf<double> d_tmp, d_w;
     dbuf<int32_t> d_flag;
 
+    // inverse-distance neighbour tables, one per forcing variable, cached by
+    // (model, parameters, source geometry)
+    struct idw_table {
+        std::vector<double> key;
+        dbuf<int32_t> idx, cnt;
+        dbuf<double> w, aux;
+        int K = 0;
+    } idw[N_FORCING];
+    dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
+    bool dst_dirty = true;
+
     size_t n_series() const { return collect == COLLECT_ALL ? PTGSK_NR : (collect == COLLECT_DISCHARGE_SNOW ? 4 : 2); }
     size_t n_state_fields() const { return PTGSK_NS; }
     size_t n_ref_params() const { return PTGSK_NP_REF; }
@@ -359,6 +370,8 @@ int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* r
         update_ix_to_id_mapping(h);
         h->has_geo = true;
         h->derived_dirty = true;
+        h->dst_dirty = true;
+        for (auto& t : h->idw) t.key.clear();
     });
 }
 
@@ -530,6 +543,97 @@ int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cel
                                            h->stream),
                   "synthetic_forcing");
         hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const double* src_xyz, const double* src_values,
+                          size_t step0, size_t n, const double* idw_param) {
+    if (!h || !src_xyz || !src_values || !idw_param) return fail(h, "shyft_hip_interpolate: null argument");
+    return guarded(h, [&] {
+        if (var < 0 || var >= N_FORCING) throw std::runtime_error("interpolate: invalid variable");
+        if (!h->has_geo) throw std::runtime_error("interpolate: geo_cell_data not set");
+        if (n_sources == 0) throw std::runtime_error("interpolate: no sources");
+        check_window(h, step0, n, "interpolate");
+        const size_t N = h->n;
+        double* out = h->d_forcing.p + (size_t(var) * h->TW + (step0 - h->w0)) * N;
+        const uint8_t* active = h->active.empty() ? nullptr : h->d_active.p;
+        h->d_src_vals.alloc(std::max(h->d_src_vals.n, n * n_sources));
+        hip_check(hipMemcpyAsync(h->d_src_vals.p, src_values, n * n_sources * sizeof(double), hipMemcpyHostToDevice,
+                                 h->stream),
+                  "upload source values");
+        if (var == FV_TEMPERATURE && n_sources == 1) {
+            // one temperature source: copied to the cells (region_model.h:470-481)
+            hip_check(launch_copy_source(h->d_src_vals.p, int(n), int(N), active, out, h->stream), "copy_source");
+            hip_check(hipStreamSynchronize(h->stream), "sync");
+            return;
+        }
+        static const int kind_of_var[N_FORCING] = {IDW_TEMPERATURE, IDW_PRECIPITATION, IDW_WIND_SPEED, IDW_REL_HUM,
+                                                    IDW_RADIATION};
+        const int kind = kind_of_var[var];
+        const int K = int(idw_param[0]);
+        if (K < 1 || K > IDW_KMAX)
+            throw std::runtime_error("interpolate: max_members must be in [1, " + std::to_string(IDW_KMAX) + "]");
+        if (h->dst_dirty) {
+            std::vector<double> xyz(3 * N), slope(N);
+            for (size_t i = 0; i < N; ++i) {
+                for (int k = 0; k < 3; ++k) xyz[3 * i + k] = h->geo[i * 11 + k];
+                slope[i] = h->geo[i * 11 + 5];
+            }
+            h->d_dst_xyz.alloc(3 * N);
+            h->d_slope.alloc(N);
+            hip_check(hipMemcpy(h->d_dst_xyz.p, xyz.data(), 3 * N * sizeof(double), hipMemcpyHostToDevice), "upload dst");
+            hip_check(hipMemcpy(h->d_slope.p, slope.data(), N * sizeof(double), hipMemcpyHostToDevice), "upload slope");
+            h->dst_dirty = false;
+        }
+        auto& tab = h->idw[var];
+        std::vector<double> key = {double(kind), double(n_sources), idw_param[0], idw_param[1], idw_param[2],
+                                   idw_param[3], idw_param[6]};
+        key.insert(key.end(), src_xyz, src_xyz + 3 * n_sources);
+        h->d_src_xyz.alloc(std::max(h->d_src_xyz.n, 3 * n_sources));
+        hip_check(hipMemcpyAsync(h->d_src_xyz.p, src_xyz, 3 * n_sources * sizeof(double), hipMemcpyHostToDevice, h->stream),
+                  "upload source xyz");
+        if (key != tab.key) {
+            tab.idx.alloc(size_t(K) * N);
+            tab.w.alloc(size_t(K) * N);
+            tab.aux.alloc(size_t(K) * N);
+            tab.cnt.alloc(N);
+            tab.K = K;
+            idw_nb_args nb;
+            nb.n_cells = int(N);
+            nb.n_sources = int(n_sources);
+            nb.kind = kind;
+            nb.max_members = K;
+            nb.max_distance = idw_param[1];
+            nb.distance_measure_factor = idw_param[2];
+            nb.zscale = idw_param[3];
+            nb.scale_factor = idw_param[6];
+            nb.src_xyz = h->d_src_xyz.p;
+            nb.dst_xyz = h->d_dst_xyz.p;
+            nb.idx = tab.idx.p;
+            nb.w = tab.w.p;
+            nb.aux = tab.aux.p;
+            nb.count = tab.cnt.p;
+            hip_check(launch_idw_neighbours(nb, h->stream), "idw_neighbours");
+            tab.key.swap(key);
+        }
+        idw_gather_args g;
+        g.n_cells = int(N);
+        g.n_sources = int(n_sources);
+        g.n_rows = int(n);
+        g.kind = kind;
+        g.by_equation = idw_param[5] != 0.0;
+        g.default_gradient = idw_param[4];
+        g.src_xyz = h->d_src_xyz.p;
+        g.src_values = h->d_src_vals.p;
+        g.slope = h->d_slope.p;
+        g.idx = tab.idx.p;
+        g.w = tab.w.p;
+        g.aux = tab.aux.p;
+        g.count = tab.cnt.p;
+        g.active = active;
+        g.out = out;
+        hip_check(launch_idw_gather(g, h->stream), "idw_gather");
+        hip_check(hipStreamSynchronize(h->stream), "idw");
     });
 }
 

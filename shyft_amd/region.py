@@ -104,6 +104,15 @@ class HipRegion:
         self._chk(self._L.shyft_hip_get_forcing(self.h, var, step0, n, _ptr(out), 0))
         return out
 
+    def interpolate(self, var: int, src_xyz: np.ndarray, src_values: np.ndarray, step0: int, idw_param):
+        """IDW of one forcing variable from sources (src_values [n][S] on the model axis)."""
+        xyz = np.ascontiguousarray(src_xyz, dtype=np.float64).reshape(-1, 3)
+        v = np.ascontiguousarray(src_values, dtype=np.float64).reshape(-1, xyz.shape[0])
+        p = np.ascontiguousarray(idw_param, dtype=np.float64)
+        assert p.size == 7
+        self._chk(self._L.shyft_hip_interpolate(self.h, var, xyz.shape[0], _ptr(xyz), _ptr(v), step0, v.shape[0],
+                                                _ptr(p)))
+
     def synthetic_forcing(self, seed: int, step0: int, n: int, cell_offset: int = 0):
         self._chk(self._L.shyft_hip_synthetic_forcing(self.h, seed, cell_offset, step0, n))
 

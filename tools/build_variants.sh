@@ -7,7 +7,7 @@ mkdir -p ../../tools/variants
 while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2
   rm -rf _vobj_$name; mkdir -p _vobj_$name/kernels
-  for f in region.hip kernels/ptgsk.hip kernels/stats.hip kernels/synth.hip kernels/selftest.hip; do
+  for f in $(grep "^SRCS :=" Makefile | cut -d= -f2); do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $flags -c $f -o _vobj_$name/${f%.hip}.o &
   done
   wait
