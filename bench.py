@@ -55,7 +55,47 @@ def parse():
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--idw", action="store_true",
+                    help="configs[2]: forcing interpolated each chunk by IDW from 500 stations (run_interpolation) "
+                         "instead of the per-cell generator")
     return ap.parse_args()
+
+
+# configs[2] station network: 500 stations on a 22 x 23 grid at 45 km spacing
+# covering the cell region, z in [0, 2000) m, values from the same generator (station ids offset by 2^40)
+N_STATIONS = 500
+STATION_ID0 = 1 << 40
+
+
+def station_network(world_cells):
+    from shyft_amd import synthetic
+    import math
+    W = int(math.ceil(math.sqrt(world_cells)))
+    span = W * 1000.0
+    k = np.arange(N_STATIONS)
+    gx, gy = 22, 23
+    xyz = np.zeros((N_STATIONS, 3))
+    xyz[:, 0] = (k % gx) * (span / (gx - 1))
+    xyz[:, 1] = (k // gx) * (span / (gy - 1))
+    xyz[:, 2] = synthetic.elevation(N_STATIONS, synthetic.SEED, STATION_ID0)
+    return xyz
+
+
+def station_values(xyz, step0, n):
+    from shyft_amd import synthetic
+    f = synthetic.forcing(N_STATIONS, step0, n, synthetic.SEED, cell_offset=STATION_ID0, z=xyz[:, 2])
+    return f  # [5][n][S]
+
+
+# IDW parameters in the C ABI layout: max_members, max_distance, f, zscale, default gradient,
+# gradient_by_equation, precipitation scale (inverse_distance.h:38-74 defaults)
+IDW_DEFAULTS = {
+    0: [20, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # temperature_parameter
+    1: [20, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # precipitation_parameter
+    2: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # wind_speed (parameter)
+    3: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # rel_hum
+    4: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # radiation
+}
 
 
 def dist_setup(n_gpus):
@@ -99,14 +139,21 @@ def build_region(cells, world, rank, local, chunk, n_steps_axis):
     return r
 
 
-def run_year(r, cells, rank, chunk, k_steps, seed, state0):
-    """K bench steps from Jan 1: per chunk generate forcing into HBM, then run_cells."""
+def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None):
+    """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
+    or IDW from the station network), then run_cells."""
     kernel_ms = []
     r.set_state(state0)
     for s in range(k_steps):
         step0 = s * chunk
         r.set_window(step0)
-        r.synthetic_forcing(seed, step0, chunk, cell_offset=rank * cells)
+        if stations is None:
+            r.synthetic_forcing(seed, step0, chunk, cell_offset=rank * cells)
+        else:
+            xyz, vals = stations
+            v = vals[s % len(vals)]
+            for var in range(5):
+                r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
         r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
     return kernel_ms
@@ -167,13 +214,19 @@ def main():
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
     r = build_region(cells, world, rank, local, chunk, n_axis)
     state0 = synthetic.default_ptgsk_state(cells)
+    stations = None
+    if a.idw:
+        # station series prepared on the host before timing (the reference's region_env input);
+        # each step uploads its chunk (14.6 MB) and interpolates 5 variables on the GPU
+        xyz = station_network(world * cells)
+        stations = (xyz, [station_values(xyz, s * chunk, chunk) for s in range(max(a.steps, a.warmup))])
 
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
-        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0)
+        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations)
     barrier_sync(pg, local)
     t0 = time.perf_counter()
-    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0)
+    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
@@ -195,9 +248,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (SURVEY.md §8d generator, seed 20251015; device-generated per chunk)",
+        "data": "synthetic (SURVEY.md §8d generator, seed 20251015; " +
+                ("500 stations, IDW per chunk)" if a.idw else "device-generated per chunk)"),
         "config": {
-            "workload": f"pt_gs_k region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
+            "workload": (f"pt_gs_k + inverse_distance from {N_STATIONS} stations, " if a.idw else "pt_gs_k ") +
+                        f"region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
                         f"({a.steps} chunks of {chunk}), discharge_collector, default PTGSKParameter",
             "cells_per_gpu": cells,
             "total_cells": world * cells,

@@ -1,0 +1,80 @@
+"""Multi-GPU plumbing: one process per GPU, cells sharded in contiguous ranges.
+
+run_cells has no cross-cell coupling (core/region_model.h:972-1021), so ranks
+never exchange data while the cells run. The only exchanges are where the
+reference itself aggregates over cells:
+  - catchment sums / averages (cell_statistics, core/cell_model.h:228-368;
+    region_model::catchment_discharges, core/region_model.h:873-885),
+  - river local inflow for routing (core/routing.h:344-383).
+Each rank reduces its own cells on its GPU into a small [C][T] partial; the
+partials are all-gathered (RCCL over xGMI with backend "nccl", gloo on CPU) and
+summed in rank order on every rank, so the result is identical on all ranks
+and run to run (no reduction-order nondeterminism).
+"""
+from __future__ import annotations
+
+import os
+
+
+def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """[begin, end) of the cells owned by `rank` (contiguous, sizes differ by at most one)."""
+    base, extra = divmod(n_total, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def env_rank() -> tuple[int, int, int]:
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def combine_partials(partial, group=None):
+    """Deterministic cross-rank sum of per-rank partials (a torch tensor, same shape on every
+    rank): all_gather, then add in rank order. Returns the total on every rank."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return partial.clone()
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(partial) for _ in range(world)]
+    dist.all_gather(parts, partial.contiguous(), group=group)
+    total = parts[0].clone()
+    for p in parts[1:]:
+        total += p
+    return total
+
+
+def max_over_ranks(value: float, device=None, group=None) -> float:
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def catchment_sums(region, series: int, step0: int, n: int, global_cids, group=None, device=None):
+    """Per-catchment sums of a response series over ALL ranks' cells.
+
+    global_cids: the catchment ids of the whole region, in the order wanted for
+    the result (e.g. the reference's cix order of the unsharded region). Each
+    rank sums its own cells per local catchment on its GPU, places the rows at
+    their global positions and the partials are combined in rank order.
+    Returns a torch tensor [len(global_cids)][n] on `device`."""
+    import torch
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    local = [int(c) for c in region.catchment_ids()]
+    pos = {int(c): i for i, c in enumerate(global_cids)}
+    missing = [c for c in local if c not in pos]
+    if missing:
+        raise RuntimeError(f"one or more supplied catchment_indexes does not exist:{missing[0]}")
+    part = torch.empty((len(local), n), dtype=torch.float64, device=dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+        region.catchment_sums_device(series, step0, n, part.data_ptr())
+    else:
+        part.copy_(torch.from_numpy(region.catchment_sums(series, step0, n)))
+    full = torch.zeros((len(global_cids), n), dtype=torch.float64, device=dev)
+    full[torch.tensor([pos[c] for c in local], device=dev, dtype=torch.long)] = part
+    return combine_partials(full, group)
