@@ -63,7 +63,7 @@ struct idw_nb_args {
 };
 
 struct idw_gather_args {
-    int n_cells, n_sources, n_rows, kind, by_equation;
+    int n_cells, n_sources, n_rows, kind, by_equation, max_members;
     double default_gradient;
     const double* src_xyz;     // [S][3]
     const double* src_values;  // [n_rows][S]

@@ -91,6 +91,11 @@ __global__ __launch_bounds__(128) void idw_neighbours_kernel(idw_nb_args a) {
     }
 }
 
+// The lane's neighbour list (source index, weight, transform constant and the
+// source z for the gradient) is loaded ONCE into registers (KT >= count, a
+// compile-time bound so the arrays stay in VGPRs) and reused for every row; only
+// the [row][source] values (a few KB per row, L1/L2 resident) are gathered per step.
+template <int KT>
 __global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n_cells) return;
@@ -99,41 +104,54 @@ __global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a) {
     const int kept = a.count[j];
     const int S = a.n_sources;
     const double slope = a.slope ? a.slope[j] : 0.9;
+    const bool temp = a.kind == IDW_TEMPERATURE;
+    int nidx[KT];
+    double nw[KT], naux[KT], nx[KT], ny[KT], nz[KT];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+        const bool in = k < kept;
+        const int s = in ? a.idx[k * N + j] : 0;
+        nidx[k] = s;
+        nw[k] = in ? a.w[k * N + j] : 0.0;
+        naux[k] = in ? a.aux[k * N + j] : 0.0;
+        nz[k] = (in && temp) ? a.src_xyz[3 * s + 2] : 0.0;
+        nx[k] = (in && temp && a.by_equation) ? a.src_xyz[3 * s] : 0.0;
+        ny[k] = (in && temp && a.by_equation) ? a.src_xyz[3 * s + 1] : 0.0;
+    }
     double* __restrict__ out = a.out;
     for (int r = 0; r < a.n_rows; ++r) {
         const double* __restrict__ row = a.src_values + (size_t)r * S;
+        double v[KT];
+#pragma unroll
+        for (int k = 0; k < KT; ++k) v[k] = k < kept ? row[nidx[k]] : 0.0;
         double scale = 1.0;
-        if (a.kind == IDW_TEMPERATURE) {
-            // temperature_gradient_scale_computer::compute over the valid neighbours (inverse_distance.h:305-330)
-            int n = 0, mn = -1, mx = -1;
+        if (temp) {
+            // temperature_gradient_scale_computer::compute over the valid neighbours in
+            // neighbour order (inverse_distance.h:305-330)
+            int n = 0;
             double z_mn = 0, z_mx = 0, t_mn = 0, t_mx = 0;
             double p0x = 0, p0y = 0, p0z = 0, t0 = 0;
-            double A[3][3], b[3];
-            for (int k = 0; k < kept; ++k) {
-                const int s = a.idx[k * N + j];
-                const double v = row[s];
-                if (!__builtin_isfinite(v)) continue;
-                const double sz = a.src_xyz[3 * s + 2];
+            double A[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, b[3] = {0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < KT; ++k) {
+                if (k >= kept || !__builtin_isfinite(v[k])) continue;
+                const double sz = nz[k];
                 if (n == 0) {
-                    mn = mx = 0;
                     z_mn = z_mx = sz;
-                    t_mn = t_mx = v;
+                    t_mn = t_mx = v[k];
                 } else if (sz < z_mn) {
-                    mn = n; z_mn = sz; t_mn = v;
+                    z_mn = sz; t_mn = v[k];
                 } else if (sz > z_mx) {
-                    mx = n; z_mx = sz; t_mx = v;
+                    z_mx = sz; t_mx = v[k];
                 }
                 if (a.by_equation) {
-                    const double sx = a.src_xyz[3 * s], sy = a.src_xyz[3 * s + 1];
-                    if (n == 0) { p0x = sx; p0y = sy; p0z = sz; t0 = v; }
-                    else if (n <= 3) {
-                        A[n - 1][0] = sx - p0x; A[n - 1][1] = sy - p0y; A[n - 1][2] = sz - p0z;
-                        b[n - 1] = v - t0;
-                    }
+                    if (n == 0) { p0x = nx[k]; p0y = ny[k]; p0z = sz; t0 = v[k]; }
+                    else if (n == 1) { A[0][0] = nx[k] - p0x; A[0][1] = ny[k] - p0y; A[0][2] = sz - p0z; b[0] = v[k] - t0; }
+                    else if (n == 2) { A[1][0] = nx[k] - p0x; A[1][1] = ny[k] - p0y; A[1][2] = sz - p0z; b[1] = v[k] - t0; }
+                    else if (n == 3) { A[2][0] = nx[k] - p0x; A[2][1] = ny[k] - p0y; A[2][2] = sz - p0z; b[2] = v[k] - t0; }
                 }
                 ++n;
             }
-            (void)mn; (void)mx;
             bool solved = false;
             if (a.by_equation && n > 3) {
                 // arma::solve on the 3x3 system of the first four valid points: determinant + cofactors
@@ -141,21 +159,20 @@ __global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a) {
                                    A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
                                    A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
                 if (fabs(det) > 0.0 && __builtin_isfinite(det)) {
-                    double x[3];
-                    const double i20 = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
-                    const double i21 = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
-                    const double i22 = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
                     const double i00 = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
                     const double i01 = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
                     const double i02 = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
                     const double i10 = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
                     const double i11 = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
                     const double i12 = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
-                    x[0] = i00 * b[0] + i01 * b[1] + i02 * b[2];
-                    x[1] = i10 * b[0] + i11 * b[1] + i12 * b[2];
-                    x[2] = i20 * b[0] + i21 * b[1] + i22 * b[2];
-                    if (__builtin_isfinite(x[0]) && __builtin_isfinite(x[1]) && __builtin_isfinite(x[2])) {
-                        scale = x[2];
+                    const double i20 = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+                    const double i21 = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+                    const double i22 = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+                    const double x0 = i00 * b[0] + i01 * b[1] + i02 * b[2];
+                    const double x1 = i10 * b[0] + i11 * b[1] + i12 * b[2];
+                    const double x2 = i20 * b[0] + i21 * b[1] + i22 * b[2];
+                    if (__builtin_isfinite(x0) && __builtin_isfinite(x1) && __builtin_isfinite(x2)) {
+                        scale = x2;
                         solved = true;
                     }
                 }
@@ -170,20 +187,18 @@ __global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a) {
             }
         }
         double sum_weights = 0.0, sum_weight_value = 0.0;
-        for (int k = 0; k < kept; ++k) {
-            const int s = a.idx[k * N + j];
-            const double v = row[s];
-            if (!__builtin_isfinite(v)) continue;
-            const double w = a.w[k * N + j];
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            if (k >= kept || !__builtin_isfinite(v[k])) continue;
             double tr;
             switch (a.kind) {
-                case IDW_TEMPERATURE: tr = v + scale * a.aux[k * N + j]; break;
-                case IDW_PRECIPITATION: tr = v * a.aux[k * N + j]; break;
-                case IDW_RADIATION: tr = v * slope; break;
-                default: tr = v; break;
+                case IDW_TEMPERATURE: tr = v[k] + scale * naux[k]; break;
+                case IDW_PRECIPITATION: tr = v[k] * naux[k]; break;
+                case IDW_RADIATION: tr = v[k] * slope; break;
+                default: tr = v[k]; break;
             }
-            sum_weight_value += w * tr;
-            sum_weights += w;
+            sum_weight_value += nw[k] * tr;
+            sum_weights += nw[k];
         }
         out[(size_t)r * N + j] = sum_weight_value / sum_weights;
     }
@@ -208,7 +223,12 @@ hipError_t launch_idw_neighbours(const idw_nb_args& a, hipStream_t stream) {
 
 hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
     if (a.n_cells == 0 || a.n_rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(idw_gather_kernel, dim3((a.n_cells + 255) / 256), dim3(256), 0, stream, a);
+    const dim3 grid((a.n_cells + 255) / 256), block(256);
+    // smallest register-resident list that holds max_members
+    if (a.max_members <= 8) hipLaunchKernelGGL(idw_gather_kernel<8>, grid, block, 0, stream, a);
+    else if (a.max_members <= 12) hipLaunchKernelGGL(idw_gather_kernel<12>, grid, block, 0, stream, a);
+    else if (a.max_members <= 20) hipLaunchKernelGGL(idw_gather_kernel<20>, grid, block, 0, stream, a);
+    else hipLaunchKernelGGL(idw_gather_kernel<IDW_KMAX>, grid, block, 0, stream, a);
     return hipGetLastError();
 }
 

@@ -622,6 +622,7 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
         g.n_rows = int(n);
         g.kind = kind;
         g.by_equation = idw_param[5] != 0.0;
+        g.max_members = tab.K;
         g.default_gradient = idw_param[4];
         g.src_xyz = h->d_src_xyz.p;
         g.src_values = h->d_src_vals.p;
