@@ -17,6 +17,10 @@ region_model.h:972-1021), weak scaling: each rank owns 1M cells of an
 N x 1M-cell region. Timing: barrier + synchronize around exactly K steps,
 max over ranks.
 
+--stack hbv_stack runs configs[3]'s stack (hbv_snow + hbv_soil + hbv_tank,
+core/hbv_stack.h:278-361) on 512K cells per GPU, so that --gpus 8 is the
+4M-cell C4 region.
+
 Extra fields: roofline (dominant kernel = ptgsk_run_kernel, HBM-bound
 accounting per SURVEY.md §8d, kernel time from HIP events on the region's
 stream) and cpu_baseline (the CPU oracle built with the host libm, run with the
@@ -40,9 +44,13 @@ METRIC = "cell-steps/sec (cells×timesteps/wall) for pt_gs_k at 1/2/4/8 MI355X"
 CHUNK = 730
 YEAR = 8760
 HBM_PEAK_BPS = 8.0e12            # MI355X HBM3E spec (MI355X_MICROARCH.md)
-READ_B_PER_CELL_STEP = 40        # T, P, WS, RH, RAD fp64
-WRITE_B_PER_CELL_STEP = 16       # avg_discharge, charge_m3s fp64
-STATE_B_PER_CELL_LAUNCH = 2 * 9 * 8  # state read + write once per launch
+# algorithmic HBM bytes of the dominant kernel
+STACKS = {
+    # name: (forcing bytes read per cell-step, series bytes written per cell-step, state bytes per cell per launch,
+    #        kernel name)
+    "pt_gs_k": (40, 16, 2 * 9 * 8, "ptgsk_run_kernel"),      # T P WS RH RAD in; discharge, charge out; 9 state
+    "hbv_stack": (32, 16, 2 * 22 * 8, "hbv_run_kernel"),     # wind not read (hbv_stack.h:295-301); 22 state
+}
 
 
 def parse():
@@ -50,7 +58,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--cells", type=int, default=1 << 20, help="cells per GPU (default 1,048,576)")
+    ap.add_argument("--cells", type=int, default=0,
+                    help="cells per GPU (default 1,048,576 for pt_gs_k, 524,288 for hbv_stack)")
+    ap.add_argument("--stack", choices=("pt_gs_k", "hbv_stack"), default="pt_gs_k")
     ap.add_argument("--chunk", type=int, default=CHUNK)
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
@@ -128,12 +138,19 @@ def max_over_ranks(pg, local, v: float) -> float:
     return float(t.item())
 
 
-def build_region(cells, world, rank, local, chunk, n_steps_axis):
+def stack_defaults(stack, cells):
     from shyft_amd import synthetic
-    from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_DISCHARGE
-    r = HipRegion(PT_GS_K, cells, device=local)
+    if stack == "hbv_stack":
+        return synthetic.default_hbv_parameters(), synthetic.default_hbv_state(cells)
+    return synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(cells)
+
+
+def build_region(stack, cells, world, rank, local, chunk, n_steps_axis):
+    from shyft_amd import synthetic
+    from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, COLLECT_DISCHARGE
+    r = HipRegion(HBV_STACK if stack == "hbv_stack" else PT_GS_K, cells, device=local)
     r.set_geo(synthetic.geo11(cells, n_catchments=100 * world, cell_offset=rank * cells, n_total=world * cells))
-    r.set_parameters(synthetic.default_ptgsk_parameters())
+    r.set_parameters(stack_defaults(stack, 1)[0])
     r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, n_steps_axis, chunk)
     r.set_collection(COLLECT_DISCHARGE)
     return r
@@ -159,11 +176,12 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None):
     return kernel_ms
 
 
-def cpu_baseline(n_cells, threads):
+def cpu_baseline(stack, n_cells, threads):
     """Reference-scheduler CPU run (oracle built with host libm) on n_cells x 8760."""
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K
     from tests import oracle_lib
+    run = oracle_lib.hbv_run if stack == "hbv_stack" else oracle_lib.ptgsk_run
     # forcing of the sample cells: identical bits from the device generator (tests/test_capi.py pins equality)
     g = HipRegion(PT_GS_K, n_cells, device=0)
     g.set_geo(synthetic.geo11(n_cells, n_total=1 << 20))
@@ -173,14 +191,13 @@ def cpu_baseline(n_cells, threads):
     f = np.stack([g.get_forcing(v, 0, YEAR) for v in range(5)])
     g.close()
     geo = synthetic.geo11(n_cells, n_total=1 << 20)
-    res = oracle_lib.ptgsk_run(geo, synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(n_cells),
-                               synthetic.T0_2015_US, synthetic.HOUR_US, f, ncore=threads, variant="libm")
+    p, st = stack_defaults(stack, n_cells)
+    res = run(geo, p, st, synthetic.T0_2015_US, synthetic.HOUR_US, f, ncore=threads, variant="libm")
     el = res["elapsed_s"]
     # single-core rate on a small slice
     n1 = min(200, n_cells)
-    r1 = oracle_lib.ptgsk_run(geo[:n1], synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(n1),
-                              synthetic.T0_2015_US, synthetic.HOUR_US, np.ascontiguousarray(f[:, :, :n1]), ncore=1,
-                              variant="libm")
+    r1 = run(geo[:n1], p, st[:n1], synthetic.T0_2015_US, synthetic.HOUR_US, np.ascontiguousarray(f[:, :, :n1]),
+             ncore=1, variant="libm")
     return {
         "value": n_cells * YEAR / el,
         "unit": "cell-steps/s",
@@ -210,10 +227,12 @@ def main():
     import torch  # noqa: F401  (device init / sync)
     from shyft_amd import synthetic
 
-    cells, chunk = a.cells, a.chunk
+    cells = a.cells or (1 << 19 if a.stack == "hbv_stack" else 1 << 20)
+    chunk = a.chunk
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
-    r = build_region(cells, world, rank, local, chunk, n_axis)
-    state0 = synthetic.default_ptgsk_state(cells)
+    r = build_region(a.stack, cells, world, rank, local, chunk, n_axis)
+    state0 = stack_defaults(a.stack, cells)[1]
+    read_b, write_b, state_b, kernel_name = STACKS[a.stack]
     stations = None
     if a.idw:
         # station series prepared on the host before timing (the reference's region_env input);
@@ -234,10 +253,10 @@ def main():
 
     total_cell_steps = world * cells * chunk * a.steps
     value = total_cell_steps / wall
-    bytes_per_launch = cells * chunk * (READ_B_PER_CELL_STEP + WRITE_B_PER_CELL_STEP) + cells * STATE_B_PER_CELL_LAUNCH
+    bytes_per_launch = cells * chunk * (read_b + write_b) + cells * state_b
     achieved = bytes_per_launch / (avg_kernel_ms * 1e-3)
     out = {
-        "metric": METRIC,
+        "metric": METRIC if a.stack == "pt_gs_k" else METRIC.replace("pt_gs_k", a.stack),
         "value": value,
         "unit": "cell-steps/s",
         "n_gpus": world,
@@ -251,9 +270,10 @@ def main():
         "data": "synthetic (SURVEY.md §8d generator, seed 20251015; " +
                 ("500 stations, IDW per chunk)" if a.idw else "device-generated per chunk)"),
         "config": {
-            "workload": (f"pt_gs_k + inverse_distance from {N_STATIONS} stations, " if a.idw else "pt_gs_k ") +
+            "workload": (f"{a.stack} + inverse_distance from {N_STATIONS} stations, " if a.idw else f"{a.stack} ") +
                         f"region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
-                        f"({a.steps} chunks of {chunk}), discharge_collector, default PTGSKParameter",
+                        f"({a.steps} chunks of {chunk}), discharge_collector, default "
+                        f"{'HbvParameter' if a.stack == 'hbv_stack' else 'PTGSKParameter'}",
             "cells_per_gpu": cells,
             "total_cells": world * cells,
             "steps_per_chunk": chunk,
@@ -268,15 +288,15 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_BPS,
             "traffic": None,
-            "kernel": "ptgsk_run_kernel",
+            "kernel": kernel_name,
             "algorithmic_bytes_per_launch": bytes_per_launch,
-            "note": "56 B/cell-step (40 B forcing read + 16 B discharge/charge write) + 144 B/cell state per launch; "
-                    "the kernel is fp64-VALU bound, not HBM bound (DESIGN.md)",
+            "note": f"{read_b + write_b} B/cell-step ({read_b} B forcing read + {write_b} B discharge/charge write) + "
+                    f"{state_b} B/cell state per launch (DESIGN.md)",
         },
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        out["cpu_baseline"] = cpu_baseline(a.cpu_cells, threads)
+        out["cpu_baseline"] = cpu_baseline(a.stack, a.cpu_cells, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     r.close()

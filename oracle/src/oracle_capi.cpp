@@ -191,3 +191,138 @@ extern "C" void oracle_gamma_pq(double a, double x, double* p, double* p1, doubl
     *p1 = r.p1;
     *prefix = r.prefix;
 }
+
+// ---------------------------------------------------------------- hbv_stack
+// Snow distribution row per parameter set: n_bins, s[8], intervals[8] (17 doubles).
+namespace {
+hbv_snow::parameter snow_param(const double* tx_cx_ts_lw_cfr, const double* dist17) {
+    hbv_snow::parameter p;
+    if (dist17) {
+        const size_t nb = size_t(dist17[0]);
+        p.s.assign(dist17 + 1, dist17 + 1 + nb);
+        p.intervals.assign(dist17 + 1 + hbv_stack::MAX_BINS, dist17 + 1 + hbv_stack::MAX_BINS + nb);
+    }
+    if (tx_cx_ts_lw_cfr) {
+        p.tx = tx_cx_ts_lw_cfr[0]; p.cx = tx_cx_ts_lw_cfr[1]; p.ts = tx_cx_ts_lw_cfr[2];
+        p.lw = tx_cx_ts_lw_cfr[3]; p.cfr = tx_cx_ts_lw_cfr[4];
+    }
+    return p;
+}
+}  // namespace
+
+extern "C" {
+
+double oracle_hbv_integrate(const double* f, const double* x, size_t n, double a, double b, int f_b_is_zero) {
+    return hbv_snow::integrate(f, x, n, a, b, f_b_is_zero != 0);
+}
+
+// hbv_snow::calculator::step on one flat state (hbv_stack::FLAT order, snow part only used).
+// distribute: 0 none, 1 state.distribute(p) (force), 2 distribute(p, false) (size mismatch only)
+int oracle_hbv_snow_step(const double* tx_cx_ts_lw_cfr, const double* dist17, double* flat_state, int64_t t0_us,
+                         int64_t t1_us, double prec, double temp, int distribute, double* outflow, char* err,
+                         size_t errlen) {
+    try {
+        auto p = snow_param(tx_cx_ts_lw_cfr, dist17);
+        hbv_stack::state s;
+        s.set(flat_state);
+        if (distribute) s.snow.distribute(p, distribute == 1);
+        hbv_snow::response r;
+        hbv_snow::calculator(p).step(s.snow, r, t0_us, t1_us, prec, temp);
+        s.get(flat_state);
+        *outflow = r.outflow;
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
+void oracle_hbv_soil_step(double fc, double beta, double* sm, double insoil, double act_evap, double* outflow) {
+    hbv_soil::parameter p{fc, beta};
+    hbv_soil::state s{*sm};
+    hbv_soil::response r;
+    hbv_soil::step(p, s, r, insoil, act_evap);
+    *sm = s.sm;
+    *outflow = r.outflow;
+}
+
+void oracle_hbv_tank_step(const double* uz1_kuz2_kuz1_perc_klz, double* uz, double* lz, double soil_outflow,
+                          double* outflow) {
+    const double* q = uz1_kuz2_kuz1_perc_klz;
+    hbv_tank::parameter p{q[0], q[1], q[2], q[3], q[4]};
+    hbv_tank::state s{*uz, *lz};
+    hbv_tank::response r;
+    hbv_tank::step(p, s, r, soil_outflow);
+    *uz = s.uz;
+    *lz = s.lz;
+    *outflow = r.outflow;
+}
+
+double oracle_hbv_ae(double sm, double pot, double lp, double snow_fraction) {
+    return hbv_actual_evapotranspiration::calculate_step(sm, pot, lp, snow_fraction);
+}
+
+// Run the hbv_stack region model on the CPU with the reference scheduler.
+//  params    : n_sets x 22 (hbv_stack.h:82-109 order)
+//  snow_dist : n_sets x 17 (n_bins, s[8], intervals[8]) or null = default 5-bin distribution
+//  state     : n_cells x 22 in/out (hbv_stack::FLAT order)
+//  out_main  : [2][T][n_cells]; out_full : [9][T][n_cells]; out_state : [22][T+1][n_cells]
+int oracle_hbv_run(size_t n_cells, const double* geo11, const double* params, const double* snow_dist, size_t n_sets,
+                   const int32_t* set_ix, double* state, int64_t t0_us, int64_t dt_us, size_t T, int start_step,
+                   int n_steps, const double* temp, const double* prec, const double* ws, const double* rh,
+                   const double* rad, double* out_main, double* out_full, double* out_state, int ncore,
+                   double* elapsed_s, char* err, size_t errlen) {
+    try {
+        hbv_region rm;
+        rm.time_axis = fixed_dt(t0_us, dt_us, T);
+        rm.params.resize(n_sets);
+        for (size_t k = 0; k < n_sets; ++k) {
+            rm.params[k].set(params + k * 22);
+            auto sp = snow_param(nullptr, snow_dist ? snow_dist + k * 17 : nullptr);
+            rm.params[k].snow.s = sp.s;
+            rm.params[k].snow.intervals = sp.intervals;
+        }
+        rm.cells.resize(n_cells);
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.geo = geo_cell_data::from_raw(geo11 + i * 11);
+            int32_t k = set_ix ? set_ix[i] : 0;
+            if (k < 0 || size_t(k) >= n_sets) return fail(err, errlen, "oracle_hbv_run: parameter set index out of range");
+            c.parameter = &rm.params[k];
+            c.state.set(state + i * hbv_stack::FLAT);
+            c.temp.resize(T); c.prec.resize(T); c.ws.resize(T); c.rh.resize(T); c.rad.resize(T);
+            for (size_t t = 0; t < T; ++t) {
+                c.temp[t] = temp[t * n_cells + i];
+                c.prec[t] = prec[t * n_cells + i];
+                c.ws[t] = ws[t * n_cells + i];
+                c.rh[t] = rh[t * n_cells + i];
+                c.rad[t] = rad[t * n_cells + i];
+            }
+            c.col.full = out_full != nullptr;
+            c.col.collect_state = out_state != nullptr;
+        }
+        auto t_begin = std::chrono::steady_clock::now();
+        rm.run_cells(size_t(ncore < 0 ? 0 : ncore), start_step, n_steps);
+        auto t_end = std::chrono::steady_clock::now();
+        if (elapsed_s) *elapsed_s = std::chrono::duration<double>(t_end - t_begin).count();
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.state.get(state + i * hbv_stack::FLAT);
+            for (size_t t = 0; t < T; ++t) {
+                if (out_main) {
+                    out_main[t * n_cells + i] = c.col.rc[hbv_stack::AVG_DISCHARGE][t];
+                    out_main[(T + t) * n_cells + i] = c.col.rc[hbv_stack::CHARGE_M3S][t];
+                }
+                if (out_full)
+                    for (int k = 0; k < hbv_stack::N_ALL; ++k) out_full[(size_t(k) * T + t) * n_cells + i] = c.col.rc[k][t];
+            }
+            if (out_state)
+                for (size_t k = 0; k < hbv_stack::FLAT; ++k)
+                    for (size_t t = 0; t <= T; ++t) out_state[(k * (T + 1) + t) * n_cells + i] = c.col.sc[k][t];
+        }
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
+}  // extern "C"

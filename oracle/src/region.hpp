@@ -1,7 +1,7 @@
 // ORACLE — test infrastructure only (see common.hpp header).
 //
 // region.hpp: the region_model::run_cells scheduler (core/region_model.h:578-597,
-// 972-1021) over pt_gs_k cells (core/cell_model.h:112-160), plus cell
+// 972-1021) over pt_gs_k and hbv_stack cells (core/cell_model.h:112-160), plus cell
 // statistics (core/cell_model.h:194-406).
 #pragma once
 #include <future>
@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "hbv.hpp"
 #include "ptgsk.hpp"
 
 namespace oracle {
@@ -32,9 +33,25 @@ struct ptgsk_cell {
     }
 };
 
-struct ptgsk_region {
-    std::vector<ptgsk_cell> cells;
-    std::vector<pt_gs_k::parameter> params;
+// hbv_stack cell (hbv_stack_cell_model.h:247-306)
+struct hbv_cell {
+    geo_cell_data geo;
+    const hbv_stack::parameter* parameter = nullptr;
+    hbv_stack::state state;
+    std::vector<double> temp, prec, ws, rh, rad;
+    hbv_stack::collectors col;
+    void run(const fixed_dt& ta, int start_step, int n_steps) {
+        if (parameter == nullptr) throw std::runtime_error("pt_hs_k::run with null parameter attempted");
+        col.initialize(ta.size(), start_step, n_steps, geo.area);
+        pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
+        hbv_stack::run_hbv_stack(geo, *parameter, ta, start_step, n_steps, fv, state, col);
+    }
+};
+
+template <class C, class P>
+struct region_of {
+    std::vector<C> cells;
+    std::vector<P> params;
     std::vector<bool> catchment_filter;  // indexed by catchment_ix
     fixed_dt time_axis;
     size_t ncore = std::thread::hardware_concurrency();
@@ -90,5 +107,8 @@ struct ptgsk_region {
         parallel_run(start_step, n_steps, use_ncore);
     }
 };
+
+using ptgsk_region = region_of<ptgsk_cell, pt_gs_k::parameter>;
+using hbv_region = region_of<hbv_cell, hbv_stack::parameter>;
 
 }  // namespace oracle

@@ -48,3 +48,35 @@ enum forcing_index { FV_TEMPERATURE = 0, FV_PRECIPITATION, FV_WIND_SPEED, FV_REL
 
 // collection modes
 enum collect_mode { COLLECT_DISCHARGE = 0, COLLECT_DISCHARGE_SNOW = 1, COLLECT_ALL = 2 };
+
+// ------------------------------------------------------------------ hbv_stack
+// parameter row: 22 reference values (core/hbv_stack.h:82-109 order), then the
+// hbv_snow distribution (n_bins, s[HBV_MAX_BINS], intervals[HBV_MAX_BINS]),
+// which the reference keeps in hbv_snow::parameter (hbv_snow.h:21-72).
+#define HBV_MAX_BINS 8
+enum hbv_param_index {
+    HK_FC = 0, HK_BETA, HK_LP, HK_UZ1, HK_KUZ2, HK_KUZ1, HK_PERC, HK_KLZ, HK_LW, HK_TX, HK_CX, HK_TS, HK_CFR,
+    HK_PCORR, HK_PT_ALBEDO, HK_PT_ALPHA, HK_DTF, HK_R_VELOCITY, HK_R_ALPHA, HK_R_BETA, HK_GM_DIRECT, HK_RSV_DRF,
+    HK_NB, HK_S0, HK_I0 = HK_S0 + HBV_MAX_BINS, HBV_NP = HK_I0 + HBV_MAX_BINS
+};
+#define HBV_NP_REF 22
+
+// hbv_stack state (hbv_stack.h:181-201): swe sca sm uz lz, the number of
+// distributed snow bins (0 = not yet distributed, hbv_snow.h:95-99) and the bins
+enum hbv_state_index {
+    HS_SWE = 0, HS_SCA, HS_SM, HS_UZ, HS_LZ, HS_NB, HS_SP0, HS_SW0 = HS_SP0 + HBV_MAX_BINS,
+    HBV_NS = HS_SW0 + HBV_MAX_BINS
+};
+
+// per-cell constants of hbv_stack (hbv_stack.h:311-318)
+enum hbv_cell_index { HC_GLACIER = 0, HC_DIRECT_RESPONSE, HC_LAND_FRACTION, HC_AREA, HC_GLACIER_AREA, HBV_NC };
+
+// response series (hbv all_response_collector, hbv_stack_cell_model.h:40-92, in this
+// repo's series-id order so the discharge collector is the prefix [0, 2) / [0, 4))
+enum hbv_series_index {
+    HR_AVG_DISCHARGE = 0, HR_CHARGE_M3S, HR_SNOW_SCA, HR_SNOW_SWE, HR_SNOW_OUTFLOW, HR_GLACIER_MELT, HR_AE_OUTPUT,
+    HR_PE_OUTPUT, HR_SOIL_OUTFLOW, HBV_NR
+};
+
+// per-cell error codes written by the stack kernels
+enum cell_error { ERR_NONE = 0, ERR_KIRCHNER_MAX_ITER = 1, ERR_NEGATIVE_OUTFLOW = 2 };

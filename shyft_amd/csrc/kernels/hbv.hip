@@ -1,0 +1,178 @@
+// hbv_stack cell kernel for gfx950.
+//
+// region_model::run_cells -> cell::run -> run_hbv_stack (core/region_model.h:578-597,
+// core/hbv_stack_cell_model.h:247-306, core/hbv_stack.h:278-361) for every cell
+// in ONE launch: lane = cell, the time loop inside the kernel, the cell state
+// (incl. the snow quantile bins) in registers, forcing read [step][cell] and
+// the collector series written [series][step][cell]. Wind speed is not read
+// (hbv_stack.h:295-301), so a step moves 32 B of forcing in and 16 B of
+// discharge/charge out per cell.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../device/hbv_dev.h"
+#include "../device/pt_dev.h"
+#include "../include_internal/kernels.h"
+
+using namespace shyft_dev;
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+__global__ __launch_bounds__(BLOCK) void hbv_run_kernel(const hbv_kargs a) {
+    const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= a.n_cells) return;
+    if (a.active && !a.active[cell]) return;
+    const size_t N = (size_t)a.n_cells;
+    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * HBV_NP;
+
+    hbv_snow_par sp_par;
+    sp_par.nb = (int)P[HK_NB];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+        sp_par.s[i] = P[HK_S0 + i];
+        sp_par.I[i] = P[HK_I0 + i];
+    }
+    sp_par.tx = P[HK_TX];
+    sp_par.cx = P[HK_CX];
+    sp_par.ts = P[HK_TS];
+    sp_par.lw = P[HK_LW];
+    sp_par.cfr = P[HK_CFR];
+    const double fc = P[HK_FC], beta = P[HK_BETA], lp = P[HK_LP];
+    const double uz1 = P[HK_UZ1], kuz2 = P[HK_KUZ2], kuz1 = P[HK_KUZ1], perc = P[HK_PERC], klz = P[HK_KLZ];
+    const double p_corr = P[HK_PCORR], pt_albedo = P[HK_PT_ALBEDO], pt_alpha = P[HK_PT_ALPHA], dtf = P[HK_DTF];
+    const double gm_direct = P[HK_GM_DIRECT];
+    const double gm_routed = 1 - gm_direct;
+
+    const double* __restrict__ cc = a.cellc;
+    const double glacier_fraction = cc[HC_GLACIER * N + cell];
+    const double direct_response_fraction = cc[HC_DIRECT_RESPONSE * N + cell];
+    const double land_fraction = cc[HC_LAND_FRACTION * N + cell];
+    const double cell_area_m2 = cc[HC_AREA * N + cell];
+    const double glacier_area_m2 = cc[HC_GLACIER_AREA * N + cell];
+    const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
+
+    // state -> registers
+    double* __restrict__ st = a.state;
+    double swe = st[HS_SWE * N + cell], sca = st[HS_SCA * N + cell];
+    double sm = st[HS_SM * N + cell], uz = st[HS_UZ * N + cell], lz = st[HS_LZ * N + cell];
+    double nb_state = st[HS_NB * N + cell];
+    double sp[MB], sw[MB];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+        sp[i] = st[(HS_SP0 + i) * N + cell];
+        sw[i] = st[(HS_SW0 + i) * N + cell];
+    }
+    // state.snow.distribute(parameter.snow, false) (hbv_stack.h:310): only on a bin-count mismatch
+    if ((int)nb_state != sp_par.nb) {
+        hbv_distribute(sp_par, sp, sw, swe, sca);
+        nb_state = (double)sp_par.nb;
+    }
+    int32_t err = 0;
+
+    const size_t TW = (size_t)a.win_len;
+    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * N;
+    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * N;
+    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * N;
+    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * N;
+    double* __restrict__ R = a.resp;
+    const size_t RS = TW * N;
+    double* __restrict__ SS = a.state_series;
+    const size_t SSS = (TW + 1) * N;
+
+    auto collect_state = [&](size_t wi) {  // state_collector::collect (hbv_stack_cell_model.h:196-212)
+        const size_t o = wi * N + cell;
+        SS[HS_SWE * SSS + o] = swe;
+        SS[HS_SCA * SSS + o] = sca;
+        SS[HS_SM * SSS + o] = sm;
+        SS[HS_UZ * SSS + o] = uz;
+        SS[HS_LZ * SSS + o] = lz;
+        SS[HS_NB * SSS + o] = nb_state;
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+            SS[(HS_SP0 + i) * SSS + o] = sp[i];
+            SS[(HS_SW0 + i) * SSS + o] = sw[i];
+        }
+    };
+
+    const int i_end = a.step0 + a.n_steps;
+    for (int i = a.step0; i < i_end; ++i) {
+        const size_t wi = (size_t)(i - a.win0);
+        const size_t fo = wi * N + cell;
+        const double temp = f_temp[fo];
+        const double rad = f_rad[fo];
+        const double rel_hum = f_rh[fo];
+        const double prec = f_prec[fo] * p_corr;
+        if (SS) collect_state(wi);
+        const double snow_outflow =
+            hbv_snow_step(sp_par, sp, sw, swe, sca, a.step_in_days, a.dt_hours, prec, temp, err);
+        // glacier_melt::step (glacier_melt.h:47-52) on the snow covered area after the snow step
+        const double sca_area = cell_area_m2 * sca;
+        double gm_melt_m3s = 0.0;
+        if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
+            gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
+        const double pot_evap = pt_pot_evap(pt_albedo, pt_alpha, temp, rad, rel_hum) * 3600.0;
+        // hbv_actual_evapotranspiration::calculate_step (hbv_actual_evapotranspiration.h:32-38)
+        const double snow_fraction = smax(sca, glacier_fraction);
+        const double ae = (1.0 - snow_fraction) * (sm < lp ? pot_evap * (sm / lp) : pot_evap);
+        const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
+        // hbv_soil::step (hbv_soil.h:55-64)
+        const double soil_temp = sm + snow_outflow;
+        const double soil_q = snow_outflow * dpow(soil_temp / fc, beta);
+        const double soil_outflow = soil_q > soil_temp ? soil_temp : soil_q;
+        sm = smax(0.0, sm + snow_outflow - soil_outflow - ae);
+        // hbv_tank::step (hbv_tank.h:64-80)
+        const double tank_in = soil_outflow + gm_routed * gm_mmh;
+        const double tank_temp = uz + tank_in;
+        const double q12 = smax(0.0, (tank_temp - uz1) * kuz2);
+        const double q11 = smin(tank_temp, uz1) * kuz1;
+        uz = uz + tank_in - perc - (q12 + q11);
+        const double q2 = (lz + perc) * klz;
+        lz = lz + perc - q2;
+        const double tank_outflow = q12 + q11 + q2;
+
+        const double total_discharge = smax(0.0, prec - ae) * direct_response_fraction + gm_direct * gm_mmh +
+                                       tank_outflow * land_fraction;
+        const double charge_m3s = +(cell_area_m2 * prec * mmh_to_m3s_scale_factor) -
+                                  (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
+                                  (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        R[HR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
+        R[HR_CHARGE_M3S * RS + fo] = charge_m3s;
+        if (a.collect >= 1) {
+            // response.snow.snow_state is never written by hbv_snow::step (hbv_snow.h:121-124): the
+            // reference collects its default (swe = sca = 0)
+            R[HR_SNOW_SCA * RS + fo] = 0.0;
+            R[HR_SNOW_SWE * RS + fo] = 0.0;
+        }
+        if (a.collect >= 2) {
+            R[HR_SNOW_OUTFLOW * RS + fo] = cell_area_m2 * snow_outflow * mmh_to_m3s_scale_factor;
+            R[HR_GLACIER_MELT * RS + fo] = gm_melt_m3s;
+            R[HR_AE_OUTPUT * RS + fo] = ae;
+            R[HR_PE_OUTPUT * RS + fo] = pot_evap;
+            R[HR_SOIL_OUTFLOW * RS + fo] = soil_outflow;
+        }
+        if (SS && i + 1 == i_end) collect_state(wi + 1);
+    }
+    st[HS_SWE * N + cell] = swe;
+    st[HS_SCA * N + cell] = sca;
+    st[HS_SM * N + cell] = sm;
+    st[HS_UZ * N + cell] = uz;
+    st[HS_LZ * N + cell] = lz;
+    st[HS_NB * N + cell] = nb_state;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+        st[(HS_SP0 + i) * N + cell] = sp[i];
+        st[(HS_SW0 + i) * N + cell] = sw[i];
+    }
+    if (err) a.err[cell] = err;
+}
+
+}  // namespace
+
+hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream) {
+    const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(hbv_run_kernel, dim3(grid), dim3(BLOCK), 0, stream, a);
+    return hipGetLastError();
+}

@@ -24,8 +24,6 @@ using namespace shyft_dev;
 
 namespace {
 
-// error codes written to err[cell]
-constexpr int32_t ERR_KIRCHNER_MAX_ITER = 1;
 #ifndef SHYFT_BLOCK
 #define SHYFT_BLOCK 256
 #endif

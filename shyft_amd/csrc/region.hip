@@ -102,7 +102,7 @@ struct shyft_hip_region {
     std::vector<size_t> cix;           // per cell
     std::vector<int64_t> cix_to_cid;   // region_model::cix_to_cid
     std::map<int64_t, size_t> cid_to_cix;
-    std::vector<double> params;        // n_sets x n_ref
+    std::vector<double> params;        // n_sets x param_width()
     size_t n_sets = 0;
     std::vector<int32_t> set_ix;
     std::vector<uint8_t> active;       // empty = no filter
@@ -118,7 +118,7 @@ struct shyft_hip_region {
     dbuf<int32_t> d_set_ix, d_err, d_doy, d_seg_cells, d_seg_off, d_sel;
     dbuf<int64_t> d_trel;
     dbuf<uint8_t> d_active;
-    dbuf<double> d_tmp, d_w;
+    dbuf<double> d_tmp, d_w, d_alt;
     dbuf<int32_t> d_flag;
 
     // inverse-distance neighbour tables, one per forcing variable, cached by
@@ -132,9 +132,14 @@ struct shyft_hip_region {
     dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
     bool dst_dirty = true;
 
-    size_t n_series() const { return collect == COLLECT_ALL ? PTGSK_NR : (collect == COLLECT_DISCHARGE_SNOW ? 4 : 2); }
-    size_t n_state_fields() const { return PTGSK_NS; }
-    size_t n_ref_params() const { return PTGSK_NP_REF; }
+    bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
+    size_t n_series() const {
+        if (collect == COLLECT_ALL) return hbv() ? HBV_NR : PTGSK_NR;
+        return collect == COLLECT_DISCHARGE_SNOW ? 4 : 2;
+    }
+    size_t n_state_fields() const { return hbv() ? HBV_NS : PTGSK_NS; }
+    size_t n_ref_params() const { return hbv() ? HBV_NP_REF : PTGSK_NP_REF; }
+    size_t param_width() const { return hbv() ? HBV_NP : PTGSK_NP_REF; }
 };
 
 namespace {
@@ -192,11 +197,36 @@ void update_ix_to_id_mapping(shyft_hip_region* h) {
 // derived per-set parameter rows and per-cell constants (pt_gs_k.h:347-357,
 // gamma_snow.h:85-87, :188, :340-343). Evaluated with the same expressions
 // the reference evaluates, on the host.
+void update_derived_hbv(shyft_hip_region* h) {
+    const size_t N = h->n;
+    std::vector<double> cc(HBV_NC * N);
+    for (size_t i = 0; i < N; ++i) {
+        const double* g = &h->geo[i * 11];
+        const double* p = &h->params[size_t(h->set_ix[i]) * HBV_NP];
+        const double glacier = g[6], reservoir = g[8];
+        const double direct = glacier * p[HK_GM_DIRECT] + reservoir * p[HK_RSV_DRF];
+        cc[HC_GLACIER * N + i] = glacier;
+        cc[HC_DIRECT_RESPONSE * N + i] = direct;
+        cc[HC_LAND_FRACTION * N + i] = 1 - direct;
+        cc[HC_AREA * N + i] = g[3];
+        cc[HC_GLACIER_AREA * N + i] = g[3] * glacier;
+    }
+    h->d_params.alloc(h->params.size());
+    h->d_cellc.alloc(cc.size());
+    h->d_set_ix.alloc(N);
+    hip_check(hipMemcpy(h->d_params.p, h->params.data(), h->params.size() * sizeof(double), hipMemcpyHostToDevice),
+              "upload params");
+    hip_check(hipMemcpy(h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
+    hip_check(hipMemcpy(h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
+    h->derived_dirty = false;
+}
+
 void update_derived(shyft_hip_region* h) {
     if (!h->derived_dirty) return;
     if (!h->has_geo) throw std::runtime_error("region: geo_cell_data not set");
     if (!h->has_params) throw std::runtime_error("region: parameters not set");
     if (h->dt <= 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
+    if (h->hbv()) return update_derived_hbv(h);
     const size_t N = h->n;
     const double dt_s = double(h->dt) / 1e6;
     const double dt_in_days = dt_s / 86400.0;
@@ -252,7 +282,7 @@ void alloc_window(shyft_hip_region* h) {
     h->d_resp.alloc(h->n_series() * h->TW * N);
     hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill resp");
     if (h->collect_state) {
-        h->d_state_series.alloc(PTGSK_NS * (h->TW + 1) * N);
+        h->d_state_series.alloc(h->n_state_fields() * (h->TW + 1) * N);
         hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill state series");
     } else {
         h->d_state_series.release();
@@ -310,7 +340,8 @@ const char* shyft_hip_last_error(const shyft_hip_region* h) { return h ? h->err.
 int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_region** out) {
     if (!out) return fail(nullptr, "shyft_hip_region_create: out is null");
     *out = nullptr;
-    if (stack != SHYFT_HIP_PT_GS_K) return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
+    if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK)
+        return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
     if (n_cells == 0 || n_cells > (size_t)INT32_MAX) return fail(nullptr, "shyft_hip_region_create: invalid n_cells");
     std::unique_ptr<shyft_hip_region> h(new shyft_hip_region());
     h->stack = stack;
@@ -322,7 +353,7 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
         hip_check(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
         hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
         hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
-        h->d_state.alloc(PTGSK_NS * n_cells);
+        h->d_state.alloc(h->n_state_fields() * n_cells);
         h->d_err.alloc(n_cells);
         h->d_flag.alloc(1);
         hip_check(hipMemset(h->d_err.p, 0, n_cells * sizeof(int32_t)), "memset");
@@ -368,6 +399,10 @@ int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* r
         if (routing_id) h->routing_id.assign(routing_id, routing_id + h->n);
         if (routing_distance) h->routing_distance.assign(routing_distance, routing_distance + h->n);
         update_ix_to_id_mapping(h);
+        std::vector<double> z(h->n);
+        for (size_t i = 0; i < h->n; ++i) z[i] = h->geo[i * 11 + 2];
+        h->d_alt.alloc(h->n);
+        hip_check(hipMemcpy(h->d_alt.p, z.data(), h->n * sizeof(double), hipMemcpyHostToDevice), "upload z");
         h->has_geo = true;
         h->derived_dirty = true;
         h->dst_dirty = true;
@@ -379,8 +414,13 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
                              const int32_t* set_ix) {
     if (!h || !params) return fail(h, "shyft_hip_set_parameters: null argument");
     return guarded(h, [&] {
-        if (n_per_set != h->n_ref_params())
+        const size_t width = h->param_width();
+        if (h->hbv()) {
+            if (n_per_set != HBV_NP_REF && n_per_set != HBV_NP)
+                throw std::runtime_error("HBV_Stack Parameter Accessor: .set size missmatch");
+        } else if (n_per_set != h->n_ref_params()) {
             throw std::runtime_error("PTGSK Parameter Accessor: .set size missmatch");
+        }
         if (n_sets == 0) throw std::runtime_error("shyft_hip_set_parameters: n_sets == 0");
         std::vector<int32_t> ix(h->n, 0);
         if (set_ix) {
@@ -390,7 +430,27 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
                 ix[i] = set_ix[i];
             }
         }
-        h->params.assign(params, params + n_sets * n_per_set);
+        h->params.assign(n_sets * width, 0.0);
+        for (size_t k = 0; k < n_sets; ++k) {
+            double* q = &h->params[k * width];
+            for (size_t j = 0; j < n_per_set; ++j) q[j] = params[k * n_per_set + j];
+            if (h->hbv() && n_per_set == HBV_NP_REF) {
+                // hbv_snow::parameter() default distribution: s = 1 (normalised mean of ones is exactly 1),
+                // quantiles 0, .25, .5, .75, 1 (hbv_snow.h:29-41)
+                static const double I5[5] = {0.0, 0.25, 0.5, 0.75, 1.0};
+                q[HK_NB] = 5.0;
+                for (int b = 0; b < 5; ++b) {
+                    q[HK_S0 + b] = 1.0;
+                    q[HK_I0 + b] = I5[b];
+                }
+            }
+            if (h->hbv()) {
+                const double nb = q[HK_NB];
+                if (!(nb >= 2.0 && nb <= double(HBV_MAX_BINS)) || nb != double(int(nb)))
+                    throw std::runtime_error("hbv_snow: number of snow bins must be in [2, " +
+                                             std::to_string(HBV_MAX_BINS) + "]");
+            }
+        }
         h->n_sets = n_sets;
         h->set_ix.swap(ix);
         h->has_params = true;
@@ -453,7 +513,7 @@ int shyft_hip_set_collection(shyft_hip_region* h, int collect, int collect_state
             h->d_resp.alloc(h->n_series() * h->TW * N);
             hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill resp");
             if (h->collect_state) {
-                h->d_state_series.alloc(PTGSK_NS * (h->TW + 1) * N);
+                h->d_state_series.alloc(h->n_state_fields() * (h->TW + 1) * N);
                 hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill");
             } else {
                 h->d_state_series.release();
@@ -537,8 +597,8 @@ int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cel
     if (!h) return fail(h, "shyft_hip_synthetic_forcing: null handle");
     return guarded(h, [&] {
         check_window(h, step0, n, "synthetic_forcing");
-        update_derived(h);  // altitude row of the cell constants
-        const double* z = h->d_cellc.p + size_t(PC_ALTITUDE) * h->n;
+        if (!h->has_geo) throw std::runtime_error("synthetic_forcing: geo_cell_data not set");
+        const double* z = h->d_alt.p;
         hip_check(launch_synthetic_forcing(h->d_forcing.p, h->TW, step0 - h->w0, n, h->n, seed, cell_offset, step0, z,
                                            h->stream),
                   "synthetic_forcing");
@@ -649,6 +709,31 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     size_t b = n_steps > 0 ? size_t(start_step) : 0;
     size_t e = n_steps > 0 ? size_t(start_step + n_steps) : h->T;
     check_window(h, b, e - b, "run_cells");
+    if (h->hbv()) {
+        hbv_kargs a;
+        a.n_cells = int(h->n);
+        a.step0 = int(b);
+        a.n_steps = int(e - b);
+        a.win0 = int(h->w0);
+        a.win_len = int(h->TW);
+        a.collect = h->collect;
+        const double dt_s = double(h->dt) / 1e6;  // to_seconds(t1 - t0)
+        a.step_in_days = dt_s / 86400.0;
+        a.dt_hours = dt_s / 3600.0;
+        a.params = h->d_params.p;
+        a.set_ix = h->d_set_ix.p;
+        a.cellc = h->d_cellc.p;
+        a.state = h->d_state.p;
+        a.forcing = h->d_forcing.p;
+        a.resp = h->d_resp.p;
+        a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
+        a.active = h->active.empty() ? nullptr : h->d_active.p;
+        a.err = h->d_err.p;
+        hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
+        hip_check(launch_hbv_run(a, h->stream), "hbv_run_kernel launch");
+        hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
+        return;
+    }
     ptgsk_kargs a;
     a.n_cells = int(h->n);
     a.step0 = int(b);
@@ -676,7 +761,7 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
 }
 
 static void finish_run(shyft_hip_region* h) {
-    hip_check(hipStreamSynchronize(h->stream), "ptgsk_run_kernel");
+    hip_check(hipStreamSynchronize(h->stream), h->hbv() ? "hbv_run_kernel" : "ptgsk_run_kernel");
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
     h->last_ms = ms;
@@ -686,6 +771,9 @@ static void finish_run(shyft_hip_region* h) {
     for (size_t i = 0; i < h->n; ++i)
         if (errs[i]) {
             hip_check(hipMemset(h->d_err.p, 0, h->n * sizeof(int32_t)), "memset");
+            if (errs[i] == ERR_NEGATIVE_OUTFLOW)
+                throw std::runtime_error("Negative outflow: total_water - swe < -1e-6 in hbv_snow (cell " +
+                                         std::to_string(i) + ")");
             throw std::runtime_error("kirchner: Max number of iterations exceeded (500). A new step size was not found. (cell " +
                                      std::to_string(i) + ")");
         }
@@ -741,7 +829,7 @@ int shyft_hip_get_state_series(const shyft_hip_region* hc, int field, size_t ste
     if (!h || !dst) return fail(h, "shyft_hip_get_state_series: null argument");
     return guarded(h, [&] {
         if (!h->collect_state) throw std::runtime_error("get_state_series: state collection is off");
-        if (field < 0 || field >= PTGSK_NS) throw std::runtime_error("get_state_series: invalid field");
+        if (field < 0 || size_t(field) >= h->n_state_fields()) throw std::runtime_error("get_state_series: invalid field");
         if (step0 < h->w0 || step0 + n > h->w0 + h->TW + 1) throw std::runtime_error("get_state_series: outside window");
         const double* src = h->d_state_series.p + (size_t(field) * (h->TW + 1) + (step0 - h->w0)) * h->n;
         copy_rows(h->stream, dst, src, n * h->n * sizeof(double), dst_on_device, 1);

@@ -20,9 +20,15 @@ PTGSK_SERIES = ("avg_discharge", "charge_m3s", "snow_sca", "snow_swe", "snow_out
                 "pe_output")
 PTGSK_STATE = ("albedo", "lwc", "surface_heat", "alpha", "sdc_melt_mean", "acc_melt", "iso_pot_energy", "temp_swe",
                "kirchner_q")
+HBV_SERIES = ("avg_discharge", "charge_m3s", "snow_sca", "snow_swe", "snow_outflow", "glacier_melt", "ae_output",
+              "pe_output", "soil_outflow")
+HBV_MAX_BINS = 8
+HBV_STATE = (("swe", "sca", "soil_moisture", "tank_uz", "tank_lz", "n_bins") +
+             tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) + tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
 SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
-STACK_NPARAM = {PT_GS_K: 31}
-STACK_NSTATE = {PT_GS_K: 9}
+STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22}
+STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE)}
+STACK_NSERIES = {PT_GS_K: len(PTGSK_SERIES), HBV_STACK: len(HBV_SERIES)}
 
 
 def _ptr(a: np.ndarray | None):

@@ -112,3 +112,31 @@ def default_ptgsk_state(n_cells: int, q: float = 1.0) -> np.ndarray:
     s = np.empty((n_cells, 9), dtype=np.float64)
     s[:] = (0.4, 0.1, 30000.0, 1.26, 0.0, 0.0, 0.0, 0.0, q)
     return s
+
+
+def default_hbv_parameters() -> np.ndarray:
+    """HbvParameter() defaults in the reference get/set order (core/hbv_stack.h:82-109)."""
+    return np.array([
+        300.0, 2.0,                   # soil.fc soil.beta (hbv_soil.h:19-24)
+        150.0,                        # ae.lp (hbv_actual_evapotranspiration.h:13-16)
+        25.0, 0.5, 0.3, 0.8, 0.02,    # tank uz1 kuz2 kuz1 perc klz (hbv_tank.h:19-31)
+        0.1, 0.0, 1.0, 0.0, 0.5,      # snow lw tx cx ts cfr (hbv_snow.h:49-53)
+        1.0,                          # p_corr.scale_factor
+        0.2, 1.26,                    # pt.albedo pt.alpha
+        6.0,                          # gm.dtf
+        1.0, 7.0, 0.0,                # routing velocity alpha beta
+        0.0,                          # gm.direct_response
+        1.0,                          # msp.reservoir_direct_response_fraction
+    ], dtype=np.float64)
+
+
+HBV_MAX_BINS = 8
+HBV_NS = 6 + 2 * HBV_MAX_BINS  # swe sca sm uz lz n_bins sp[8] sw[8]
+
+
+def default_hbv_state(n_cells: int, uz: float = 40.0, lz: float = 40.0) -> np.ndarray:
+    """HbvState() (hbv_stack.h:181-190: snow swe = sca = 0 undistributed, soil sm 0) with tank uz, lz."""
+    s = np.zeros((n_cells, HBV_NS), dtype=np.float64)
+    s[:, 3] = uz
+    s[:, 4] = lz
+    return s

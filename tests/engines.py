@@ -1,4 +1,4 @@
-"""Run one small pt_gs_k region on either engine with the same call:
+"""Run one small pt_gs_k or hbv_stack region on either engine with the same call:
 'oracle' (CPU restatement, the checker) or 'hip' (the product C ABI on the GPU)."""
 from __future__ import annotations
 
@@ -48,6 +48,43 @@ def run(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_ste
             out["full"] = allser
         if collect_state:
             out["state_series"] = np.stack([r.get_state_series(k, 0, T + 1) for k in range(9)])
+        return out
+    finally:
+        r.close()
+
+
+def run_hbv(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, snow_dist=None,
+            full=True, collect_state=False):
+    """hbv_stack region; forcing [5][T][N]; params [n_sets][22]; snow_dist [n_sets][17] or None; state [N][22].
+    Returns dict main [2][T][N], full [9][T][N], state [N][22] (+ state_series [22][T+1][N])."""
+    geo11 = np.atleast_2d(geo11)
+    if engine == "oracle":
+        return oracle_lib.hbv_run(geo11, params, state, t0_us, dt_us, forcing, start_step, n_steps, set_ix,
+                                  snow_dist=snow_dist, full=full, collect_state=collect_state)
+    from shyft_amd.region import HipRegion, HBV_STACK, COLLECT_ALL, COLLECT_DISCHARGE, HBV_STATE
+    N = geo11.shape[0]
+    T = forcing.shape[1]
+    p = np.atleast_2d(np.asarray(params, dtype=np.float64))
+    if snow_dist is not None:
+        p = np.concatenate([p, np.atleast_2d(snow_dist)], axis=1)  # the 39-wide C-ABI row
+    r = HipRegion(HBV_STACK, N)
+    try:
+        r.set_geo(geo11)
+        r.set_parameters(p, set_ix)
+        r.set_time_axis(t0_us, dt_us, T)
+        r.set_collection(COLLECT_ALL if full else COLLECT_DISCHARGE, collect_state)
+        r.set_state(np.asarray(state).reshape(N, len(HBV_STATE)))
+        for v in range(5):
+            r.set_forcing(v, 0, forcing[v])
+        r.run_cells(0, start_step, n_steps)
+        out = {"state": r.get_state()}
+        ns = 9 if full else 2
+        allser = np.stack([r.get_series(k, 0, T) for k in range(ns)])
+        out["main"] = allser[:2]
+        if full:
+            out["full"] = allser
+        if collect_state:
+            out["state_series"] = np.stack([r.get_state_series(k, 0, T + 1) for k in range(len(HBV_STATE))])
         return out
     finally:
         r.close()

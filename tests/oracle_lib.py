@@ -61,6 +61,21 @@ def load(variant: str = "detmath"):
     L.oracle_ptgsk_run.argtypes = ([C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.c_int64, C.c_size_t, C.c_int, C.c_int] + [C.c_void_p] * 8 +
                                    [C.c_int, _dp, C.c_char_p, C.c_size_t])
+    L.oracle_hbv_integrate.restype = _d
+    L.oracle_hbv_integrate.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, _d, _d, C.c_int]
+    L.oracle_hbv_snow_step.restype = C.c_int
+    L.oracle_hbv_snow_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, _d, _d, C.c_int, _dp,
+                                       C.c_char_p, C.c_size_t]
+    L.oracle_hbv_soil_step.restype = None
+    L.oracle_hbv_soil_step.argtypes = [_d, _d, _dp, _d, _d, _dp]
+    L.oracle_hbv_tank_step.restype = None
+    L.oracle_hbv_tank_step.argtypes = [C.c_void_p, _dp, _dp, _d, _dp]
+    L.oracle_hbv_ae.restype = _d
+    L.oracle_hbv_ae.argtypes = [_d] * 4
+    L.oracle_hbv_run.restype = C.c_int
+    L.oracle_hbv_run.argtypes = ([C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                  C.c_int64, C.c_int64, C.c_size_t, C.c_int, C.c_int] + [C.c_void_p] * 8 +
+                                 [C.c_int, _dp, C.c_char_p, C.c_size_t])
     _CACHE[variant] = L
     return L
 
@@ -97,3 +112,82 @@ def ptgsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps
     if collect_state:
         r["state_series"] = out_state
     return r
+
+
+HBV_MAX_BINS = 8
+HBV_FLAT = 6 + 2 * HBV_MAX_BINS   # swe sca sm uz lz n_bins sp[8] sw[8]
+
+
+def hbv_normalize(s, intervals):
+    """hbv_snow::parameter::normalize_snow_distribution (hbv_snow.h:42-47) as set_snow_redistribution_factors
+    applies it: s / integrate(s, intervals, n, intervals[0], intervals[-1])."""
+    L = load()
+    f = np.ascontiguousarray(s, dtype=np.float64)
+    x = np.ascontiguousarray(intervals, dtype=np.float64)
+    mean = L.oracle_hbv_integrate(f.ctypes.data_as(C.c_void_p), x.ctypes.data_as(C.c_void_p), len(x), float(x[0]),
+                                  float(x[-1]), 0)
+    return f / mean
+
+
+def hbv_dist_row(s, intervals):
+    """(n_bins, s[8], intervals[8]) row of one parameter set's snow distribution."""
+    row = np.zeros(1 + 2 * HBV_MAX_BINS)
+    n = len(s)
+    row[0] = n
+    row[1:1 + n] = s
+    row[1 + HBV_MAX_BINS:1 + HBV_MAX_BINS + n] = intervals
+    return row
+
+
+def hbv_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, snow_dist=None,
+            full=False, collect_state=False, ncore=0, variant="detmath"):
+    """Run the oracle hbv_stack region. params [n_sets][22]; snow_dist [n_sets][17] or None (default 5 bins);
+    state [N][22]. Returns dict main [2][T][N], full [9][T][N], state_series [22][T+1][N], state [N][22]."""
+    L = load(variant)
+    geo11 = np.ascontiguousarray(geo11, dtype=np.float64)
+    N = geo11.shape[0]
+    params = np.ascontiguousarray(np.atleast_2d(params), dtype=np.float64)
+    dist = None if snow_dist is None else np.ascontiguousarray(np.atleast_2d(snow_dist), dtype=np.float64)
+    st = np.ascontiguousarray(state, dtype=np.float64).reshape(N, HBV_FLAT).copy()
+    F = np.ascontiguousarray(forcing, dtype=np.float64)
+    T = F.shape[1]
+    ix = None if set_ix is None else np.ascontiguousarray(set_ix, dtype=np.int32)
+    out_main = np.empty((2, T, N))
+    out_full = np.empty((9, T, N)) if full else None
+    out_state = np.empty((HBV_FLAT, T + 1, N)) if collect_state else None
+    el = C.c_double(0.0)
+    err = C.create_string_buffer(512)
+    rc = L.oracle_hbv_run(N, _p(geo11), _p(params), _p(dist), params.shape[0], _p(ix), _p(st), int(t0_us), int(dt_us),
+                          T, int(start_step), int(n_steps), _p(F[0]), _p(F[1]), _p(F[2]), _p(F[3]), _p(F[4]),
+                          _p(out_main), _p(out_full), _p(out_state), int(ncore), C.byref(el), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    r = {"main": out_main, "state": st, "elapsed_s": el.value}
+    if full:
+        r["full"] = out_full
+    if collect_state:
+        r["state_series"] = out_state
+    return r
+
+
+def hbv_snow_step(flat_state, prec, temp, t0_us=0, t1_us=3600_000_000, s=None, intervals=None, tx=0.0, cx=1.0,
+                  ts=0.0, lw=0.1, cfr=0.5, distribute=0, variant="detmath"):
+    """One hbv_snow::calculator::step; returns (new flat state, outflow)."""
+    L = load(variant)
+    st = np.ascontiguousarray(flat_state, dtype=np.float64).copy()
+    dist = None if s is None else hbv_dist_row(s, intervals)
+    pv = np.array([tx, cx, ts, lw, cfr], dtype=np.float64)
+    out = C.c_double(0.0)
+    err = C.create_string_buffer(512)
+    rc = L.oracle_hbv_snow_step(_p(pv), _p(dist), _p(st), int(t0_us), int(t1_us), float(prec), float(temp),
+                                int(distribute), C.byref(out), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    return st, out.value
+
+
+def hbv_snow_state(swe=0.0, sca=0.0, sm=0.0, uz=20.0, lz=10.0):
+    """flat hbv state (HbvState() defaults: soil sm 0, tank uz 20 lz 10, undistributed snow)."""
+    v = np.zeros(HBV_FLAT)
+    v[:5] = [swe, sca, sm, uz, lz]
+    return v
