@@ -211,6 +211,20 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
+def pmc_traffic(stack, cells, chunk):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/r01/<stack>_pmc.json, FETCH_SIZE + WRITE_SIZE, tools/gpu_profile.sh) when they were taken on
+    this exact workload; None otherwise. PMC counters cannot be read from inside this process."""
+    path = os.path.join(ROOT, "profiles", "r01", f"{stack.replace('_', '')}_pmc.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get("cells") != cells or d.get("chunk") != chunk:
+        return None
+    return d["traffic_bytes_per_launch"]
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -255,6 +269,7 @@ def main():
     value = total_cell_steps / wall
     bytes_per_launch = cells * chunk * (read_b + write_b) + cells * state_b
     achieved = bytes_per_launch / (avg_kernel_ms * 1e-3)
+    traffic_b = pmc_traffic(a.stack, cells, chunk)
     out = {
         "metric": METRIC if a.stack == "pt_gs_k" else METRIC.replace("pt_gs_k", a.stack),
         "value": value,
@@ -287,7 +302,10 @@ def main():
             "peak": HBM_PEAK_BPS / 1e9,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_BPS,
-            "traffic": None,
+            "traffic": None if traffic_b is None else traffic_b / (avg_kernel_ms * 1e-3) / 1e9,
+            "traffic_bytes_per_launch": traffic_b,
+            "traffic_source": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (profiles/r01/*_pmc.json), over this "
+                              "run's average launch duration, GB/s like achieved",
             "kernel": kernel_name,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "note": f"{read_b + write_b} B/cell-step ({read_b} B forcing read + {write_b} B discharge/charge write) + "
