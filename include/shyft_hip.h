@@ -52,6 +52,11 @@ enum shyft_hip_ptgsk_series {
     SHYFT_HIP_SNOW_OUTFLOW = 4, SHYFT_HIP_GLACIER_MELT = 5, SHYFT_HIP_AE_OUTPUT = 6, SHYFT_HIP_PE_OUTPUT = 7
 };
 
+/* series ids accepted by the statistics / cell-series entry points besides the response ids above:
+ * the cell environment (forcing) variable v as SHYFT_HIP_SERIES_FORCING + v, and state-collector
+ * field f (T+1 instant axis) as SHYFT_HIP_SERIES_STATE + f. */
+enum shyft_hip_series_base { SHYFT_HIP_SERIES_FORCING = 100, SHYFT_HIP_SERIES_STATE = 200 };
+
 /* statistics scope (core/cell_model.h:183-186 stat_scope) */
 enum shyft_hip_stat_scope { SHYFT_HIP_SCOPE_CELL_IX = 0, SHYFT_HIP_SCOPE_CATCHMENT = 1 };
 
@@ -140,7 +145,7 @@ int shyft_hip_get_state_series(const shyft_hip_region* h, int field, size_t step
 
 /* Catchment statistics (cell_statistics::sum_catchment_feature / average_catchment_feature,
  * core/cell_model.h:228-333): sum (weighted == 0) or area-weighted average (weighted != 0)
- * of series `series` over the cells selected by ids[n_ids] (scope: cell index or catchment id;
+ * of series `series` (response id, SHYFT_HIP_SERIES_FORCING + v or SHYFT_HIP_SERIES_STATE + f) over the cells selected by ids[n_ids] (scope: cell index or catchment id;
  * n_ids == 0 selects all cells), for steps [step0, step0+n). dst[n]. Throws (returns error)
  * on unknown ids like verify_cids_exist (cell_model.h:198-211). */
 int shyft_hip_statistics(const shyft_hip_region* h, int series, const int64_t* ids, size_t n_ids, int scope,
@@ -151,6 +156,20 @@ int shyft_hip_catchment_sums(const shyft_hip_region* h, int series, size_t step0
                              int dst_on_device);
 size_t shyft_hip_number_of_catchments(const shyft_hip_region* h);
 int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids);
+
+/* Deep copy of a region (cells, parameters, time axis, forcing, state, collected series) on the
+ * same device: the region_model copy constructor / clone (core/region_model.h:297-301, expose.h:147),
+ * used for create_opt_model_clone / create_full_model_clone. */
+int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out);
+
+/* One cell's view of a series (cell.env_ts.<var>, cell.rc.<series>, cell.sc.<field>,
+ * core/cell_model.h:47-81,112-160): steps [step0, step0+n) copied to/from buf[n].
+ * write != 0 is allowed for forcing only (env_ts.<var>.set(i, v)). series uses the ids above. */
+int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t step0, size_t n, double* buf, int write);
+
+/* region_model::is_cell_env_ts_ok (core/region_model.h:954-962): *ok = 1 when no forcing value of a
+ * calculated cell (catchment filter) in the resident window is NaN. */
+int shyft_hip_forcing_ok(const shyft_hip_region* h, int* ok);
 
 /* Diagnostic: evaluate one device elementary function (0 exp, 1 log, 2 pow(x, y), 3 lgamma,
  * 4 gamma_p(x, y)) on n host inputs on the current device; out[n] host. Used by the parity

@@ -1,0 +1,295 @@
+// pybind11 module shyft_amd.api._api: the Python surface of the host layer.
+//
+// The reference exposes region_model<cell_t> and its data types with
+// boost.python (api/boostpython/expose.h:98-430, api_*.cpp, pt_gs_k.cpp:34-174,
+// hbv_stack.cpp). boost.python is not available here, so this module binds the
+// same C++ host classes (host/region_model.hpp) with pybind11; the Python
+// package shyft_amd.api adds the reference's names and decorators on top
+// (shyft/api/__init__.py, shyft/api/pt_gs_k/__init__.py).
+//
+// Time crosses the boundary as seconds (int or float, like shyft's `time`);
+// internally it is int64 microseconds.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cmath>
+
+#include "region_model.hpp"
+
+namespace py = pybind11;
+using namespace shyft_hip::host;
+
+namespace {
+
+utctime to_us(double seconds) { return utctime(std::llround(seconds * 1e6)); }
+double to_s(utctime us) { return double(us) / 1e6; }
+
+template <class Stack>
+void bind_model(py::module_& m, const char* name) {
+    using M = region_model<Stack>;
+    py::class_<M>(m, name, py::dynamic_attr())
+        .def(py::init<const std::vector<geo_cell_data>&, const std::vector<double>&, bool, int>(), py::arg("geo_data_vector"),
+             py::arg("region_param"), py::arg("full_collection") = true, py::arg("device") = -1)
+        .def(py::init<const std::vector<geo_cell_data>&, const std::vector<double>&,
+                      const std::map<int64_t, std::vector<double>>&, bool>(),
+             py::arg("geo_data_vector"), py::arg("region_param"), py::arg("catchment_parameters"),
+             py::arg("full_collection") = true)
+        .def(py::init<const M&, bool>(), py::arg("other_model"), py::arg("full_collection"))
+        .def_readwrite("ncore", &M::ncore)
+        .def_readwrite("_ip_parameter", &M::ip_parameter)
+        .def_readwrite("_region_env", &M::region_env)
+        .def_readwrite("_initial_state", &M::initial_state)
+        .def_readwrite("_river_network", &M::rivers)
+        .def_property_readonly("_time_axis", [](const M& x) { return x.time_axis; })
+        .def_property_readonly("full_collection", &M::full_collection)
+        .def("size", &M::size)
+        .def("number_of_catchments", &M::number_of_catchments)
+        .def_property_readonly("catchment_ids", &M::catchment_ids)
+        .def("extract_geo_cell_data", &M::extract_geo_cell_data)
+        .def("_set_region_parameter", &M::set_region_parameter)
+        .def("_get_region_parameter", &M::get_region_parameter)
+        .def("_set_catchment_parameter", &M::set_catchment_parameter)
+        .def("_update_catchment_parameter", &M::update_catchment_parameter)
+        .def("remove_catchment_parameter", &M::remove_catchment_parameter, py::arg("catchment_id"))
+        .def("has_catchment_parameter", &M::has_catchment_parameter, py::arg("catchment_id"))
+        .def("_get_catchment_parameter", &M::get_catchment_parameter)
+        .def("set_catchment_calculation_filter", &M::set_catchment_calculation_filter, py::arg("catchment_id_list"))
+        .def("set_calculation_filter", &M::set_calculation_filter, py::arg("catchment_id_list"), py::arg("river_id_list"))
+        .def("is_calculated", &M::is_calculated, py::arg("catchment_id"))
+        .def("initialize_cell_environment", &M::initialize_cell_environment, py::arg("time_axis"))
+        .def("_interpolate", &M::interpolate)
+        .def("_run_interpolation", &M::run_interpolation)
+        .def("is_cell_env_ts_ok", &M::is_cell_env_ts_ok)
+        .def("run_cells", &M::run_cells, py::arg("use_ncore") = 0, py::arg("start_step") = 0, py::arg("n_steps") = 0,
+             py::call_guard<py::gil_scoped_release>())
+        .def("_get_states", [](const M& x) { return x.current_state(); })
+        .def("_set_states", &M::set_states)
+        .def("revert_to_initial_state", &M::revert_to_initial_state)
+        .def("adjust_q", &M::adjust_q, py::arg("q_scale"), py::arg("cids"))
+        .def("set_state_collection", &M::set_state_collection, py::arg("catchment_id"), py::arg("on_or_off"))
+        .def("set_snow_sca_swe_collection", &M::set_snow_sca_swe_collection, py::arg("catchment_id"), py::arg("on_or_off"))
+        .def("_cell_collects_state", &M::cell_collects_state)
+        .def("_cell_collects_snow", &M::cell_collects_snow)
+        .def("_cell_series", [](const M& x, int s, size_t c) { auto v = x.cell_series(s, c); return py::array_t<double>(v.size(), v.data()); })
+        .def("_cell_value", &M::cell_value)
+        .def("_set_cell_value", &M::set_cell_value)
+        .def("_set_cell_forcing", &M::set_cell_forcing)
+        .def("_cell_geo", [](const M& x, size_t i) { return x.cells_geo().at(i); })
+        .def("_cell_parameter", &M::cell_parameter)
+        .def("_stat_series", [](const M& x, int s, const std::vector<int64_t>& ids, int scope, bool w) {
+            auto v = x.stat_series(s, ids, scope, w);
+            return py::array_t<double>(v.size(), v.data());
+        })
+        .def("_stat_value", &M::stat_value)
+        .def("_stat_raster", &M::stat_raster)
+        .def("_pot_ratio_series", [](const M& x, const std::vector<int64_t>& ids, int scope) {
+            auto v = x.pot_ratio_series(ids, scope);
+            return py::array_t<double>(v.size(), v.data());
+        })
+        .def("_pot_ratio_raster", &M::pot_ratio_raster)
+        .def("_pot_ratio_value", &M::pot_ratio_value)
+        .def("_area_stat", &M::area_stat)
+        .def("_catchment_sums", &M::catchment_sums)
+        .def("connect_catchment_to_river", &M::connect_catchment_to_river, py::arg("cid"), py::arg("rid"))
+        .def("_set_cell_routing", &M::set_cell_routing)
+        .def("has_routing", &M::has_routing)
+        .def("_river_output_flow_m3s", &M::river_output_flow_m3s)
+        .def("_river_upstream_inflow_m3s", &M::river_upstream_inflow_m3s)
+        .def("_river_local_inflow_m3s", &M::river_local_inflow_m3s);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_api, m) {
+    m.doc() = "MI355X region engine host layer (C++ over the shyft_hip C ABI)";
+
+    py::class_<geo_point>(m, "GeoPoint")
+        .def(py::init<>())
+        .def(py::init<double, double, double>(), py::arg("x"), py::arg("y"), py::arg("z"))
+        .def_readwrite("x", &geo_point::x)
+        .def_readwrite("y", &geo_point::y)
+        .def_readwrite("z", &geo_point::z)
+        .def("__deepcopy__", [](const geo_point& p, py::dict) { return p; })
+        .def_static("distance2", [](const geo_point& a, const geo_point& b) {
+            return (a.x - b.x) * (a.x - b.x) + (a.y - b.y) * (a.y - b.y) + (a.z - b.z) * (a.z - b.z);
+        })
+        .def("__repr__", [](const geo_point& p) {
+            return "GeoPoint(" + std::to_string(p.x) + ", " + std::to_string(p.y) + ", " + std::to_string(p.z) + ")";
+        });
+
+    py::class_<land_type_fractions>(m, "LandTypeFractions")
+        .def(py::init<>())
+        .def(py::init<double, double, double, double, double>(), py::arg("glacier"), py::arg("lake"),
+             py::arg("reservoir"), py::arg("forest"), py::arg("unspecified"))
+        .def("glacier", &land_type_fractions::glacier)
+        .def("lake", &land_type_fractions::lake)
+        .def("reservoir", &land_type_fractions::reservoir)
+        .def("forest", &land_type_fractions::forest)
+        .def("unspecified", &land_type_fractions::unspecified)
+        .def("snow_storage", &land_type_fractions::snow_storage)
+        .def("set_fractions", &land_type_fractions::set_fractions, py::arg("glacier"), py::arg("lake"),
+             py::arg("reservoir"), py::arg("forest"));
+
+    py::class_<routing_info>(m, "RoutingInfo")
+        .def(py::init<>())
+        .def(py::init<int64_t, double>(), py::arg("id"), py::arg("distance") = 0.0)
+        .def_readwrite("id", &routing_info::id)
+        .def_readwrite("distance", &routing_info::distance);
+
+    py::class_<geo_cell_data>(m, "GeoCellData")
+        .def(py::init<>())
+        .def(py::init<const geo_point&, double, int64_t, double, const land_type_fractions&>(), py::arg("mid_point"),
+             py::arg("area"), py::arg("catchment_id"), py::arg("radiation_slope_factor") = 0.9,
+             py::arg("land_type_fractions") = land_type_fractions())
+        .def("mid_point", &geo_cell_data::mid_point)
+        .def("area", &geo_cell_data::area)
+        .def("catchment_id", &geo_cell_data::catchment_id)
+        .def("set_catchment_id", [](geo_cell_data& g, int64_t c) { g.catchment_id_ = c; })
+        .def("radiation_slope_factor", &geo_cell_data::radiation_slope_factor)
+        .def("land_type_fractions_info", [](geo_cell_data& g) -> land_type_fractions& { return g.fractions; },
+             py::return_value_policy::reference_internal)
+        .def("set_land_type_fractions", [](geo_cell_data& g, const land_type_fractions& f) { g.fractions = f; })
+        .def_readwrite("routing_info", &geo_cell_data::routing)
+        .def_readwrite("routing", &geo_cell_data::routing);
+
+    py::class_<fixed_dt>(m, "TimeAxisFixedDeltaT")
+        .def(py::init([](double t0, double dt, size_t n) { return fixed_dt(to_us(t0), to_us(dt), n); }), py::arg("start"),
+             py::arg("delta_t"), py::arg("n"))
+        .def("size", &fixed_dt::size)
+        .def("__len__", &fixed_dt::size)
+        .def_property_readonly("start", [](const fixed_dt& a) { return to_s(a.t); })
+        .def_property_readonly("delta_t", [](const fixed_dt& a) { return to_s(a.dt); })
+        .def_property_readonly("n", [](const fixed_dt& a) { return a.n; })
+        .def("time", [](const fixed_dt& a, size_t i) { return to_s(a.time(i)); })
+        .def("period", [](const fixed_dt& a, size_t i) { auto p = a.period(i); return std::make_pair(to_s(p.start), to_s(p.end)); })
+        .def("total_period", [](const fixed_dt& a) { auto p = a.total_period(); return std::make_pair(to_s(p.start), to_s(p.end)); })
+        .def("index_of", [](const fixed_dt& a, double t) { auto i = a.index_of(to_us(t)); return i == npos ? int64_t(-1) : int64_t(i); })
+        .def("__eq__", &fixed_dt::operator==);
+
+    py::enum_<ts_point_fx>(m, "point_interpretation_policy")
+        .value("POINT_INSTANT_VALUE", POINT_INSTANT_VALUE)
+        .value("POINT_AVERAGE_VALUE", POINT_AVERAGE_VALUE)
+        .export_values();
+
+    py::class_<point_ts>(m, "_PointTs")
+        .def(py::init([](const fixed_dt& ta, std::vector<double> v, ts_point_fx fx) { return point_ts(ta, std::move(v), fx); }))
+        .def(py::init([](const std::vector<double>& t, double t_end, std::vector<double> v, ts_point_fx fx) {
+            std::vector<utctime> tu(t.size());
+            for (size_t i = 0; i < t.size(); ++i) tu[i] = to_us(t[i]);
+            return point_ts(std::move(tu), to_us(t_end), std::move(v), fx);
+        }))
+        .def("__deepcopy__", [](const point_ts& s, py::dict) { return point_ts(s); })
+        .def("size", &point_ts::size)
+        .def("value", &point_ts::value)
+        .def("set", &point_ts::set)
+        .def("time", [](const point_ts& s, size_t i) { return to_s(s.time(i)); })
+        .def("point_interpretation", [](const point_ts& s) { return s.fx; })
+        .def("total_period", [](const point_ts& s) { auto p = s.total_period(); return std::make_pair(to_s(p.start), to_s(p.end)); })
+        .def("__call__", [](const point_ts& s, double t) { return s(to_us(t)); })
+        .def_property_readonly("_values", [](const point_ts& s) { return py::array_t<double>(s.v.size(), s.v.data()); })
+        .def_property_readonly("_times", [](const point_ts& s) {
+            std::vector<double> t(s.t.size());
+            for (size_t i = 0; i < t.size(); ++i) t[i] = to_s(s.t[i]);
+            return t;
+        })
+        .def_property_readonly("_t_end", [](const point_ts& s) { return to_s(s.t_end); })
+        .def("average", [](const point_ts& s, const fixed_dt& ta) {
+            auto v = average_values(s, ta);
+            return py::array_t<double>(v.size(), v.data());
+        });
+
+    py::class_<geo_point_ts>(m, "_GeoPointTs")
+        .def(py::init([](const geo_point& p, const point_ts& ts) { return geo_point_ts{p, ts, ""}; }))
+        .def_readwrite("_mid_point", &geo_point_ts::mid_point)
+        .def_readwrite("_ts", &geo_point_ts::ts)
+        .def_readwrite("uid", &geo_point_ts::uid);
+
+    py::class_<region_environment>(m, "_RegionEnvironment")
+        .def(py::init<>())
+        .def_readwrite("temperature", &region_environment::temperature)
+        .def_readwrite("precipitation", &region_environment::precipitation)
+        .def_readwrite("wind_speed", &region_environment::wind_speed)
+        .def_readwrite("rel_hum", &region_environment::rel_hum)
+        .def_readwrite("radiation", &region_environment::radiation);
+
+    py::class_<idw_parameter>(m, "IDWParameter")
+        .def(py::init<>())
+        .def(py::init([](size_t mm, double md, double f, double zs) {
+                 idw_parameter p; p.max_members = mm; p.max_distance = md; p.distance_measure_factor = f; p.zscale = zs;
+                 return p;
+             }),
+             py::arg("max_members") = 10, py::arg("max_distance") = 200000.0, py::arg("distance_measure_factor") = 2.0,
+             py::arg("zscale") = 1.0)
+        .def_readwrite("max_members", &idw_parameter::max_members)
+        .def_readwrite("max_distance", &idw_parameter::max_distance)
+        .def_readwrite("distance_measure_factor", &idw_parameter::distance_measure_factor)
+        .def_readwrite("zscale", &idw_parameter::zscale);
+    py::class_<idw_temperature_parameter, idw_parameter>(m, "IDWTemperatureParameter")
+        .def(py::init<>())
+        .def(py::init([](double g, size_t mm, double md, bool eq) {
+                 idw_temperature_parameter p; p.default_temp_gradient = g; p.max_members = mm; p.max_distance = md;
+                 p.gradient_by_equation = eq; return p;
+             }),
+             py::arg("default_gradient") = -0.006, py::arg("max_members") = 20, py::arg("max_distance") = 200000.0,
+             py::arg("gradient_by_equation") = false)
+        .def_readwrite("default_temp_gradient", &idw_temperature_parameter::default_temp_gradient)
+        .def_readwrite("gradient_by_equation", &idw_temperature_parameter::gradient_by_equation);
+    py::class_<idw_precipitation_parameter, idw_parameter>(m, "IDWPrecipitationParameter")
+        .def(py::init<>())
+        .def(py::init([](double s, size_t mm, double md) {
+                 idw_precipitation_parameter p; p.scale_factor = s; p.max_members = mm; p.max_distance = md; return p;
+             }),
+             py::arg("scale_factor") = 1.02, py::arg("max_members") = 20, py::arg("max_distance") = 200000.0)
+        .def_readwrite("scale_factor", &idw_precipitation_parameter::scale_factor);
+    py::class_<interpolation_parameter>(m, "InterpolationParameter")
+        .def(py::init<>())
+        .def_readwrite("use_idw_for_temperature", &interpolation_parameter::use_idw_for_temperature)
+        .def_readwrite("temperature_idw", &interpolation_parameter::temperature_idw)
+        .def_readwrite("precipitation", &interpolation_parameter::precipitation)
+        .def_readwrite("wind_speed", &interpolation_parameter::wind_speed)
+        .def_readwrite("radiation", &interpolation_parameter::radiation)
+        .def_readwrite("rel_hum", &interpolation_parameter::rel_hum);
+
+    py::class_<uhg_parameter>(m, "UHGParameter")
+        .def(py::init<>())
+        .def(py::init<double, double, double>(), py::arg("velocity"), py::arg("alpha") = 7.0, py::arg("beta") = 0.0)
+        .def_readwrite("velocity", &uhg_parameter::velocity)
+        .def_readwrite("alpha", &uhg_parameter::alpha)
+        .def_readwrite("beta", &uhg_parameter::beta);
+    py::class_<river>(m, "River")
+        .def(py::init([](int64_t id, const routing_info& ds, const uhg_parameter& p) { return river(id, ds.id, ds.distance, p); }),
+             py::arg("id"), py::arg("downstream") = routing_info(), py::arg("parameter") = uhg_parameter())
+        .def_readwrite("id", &river::id)
+        .def_property("downstream", [](const river& r) { return routing_info(r.downstream_id, r.downstream_distance); },
+                      [](river& r, const routing_info& ri) { r.downstream_id = ri.id; r.downstream_distance = ri.distance; })
+        .def_readwrite("parameter", &river::parameter)
+        .def("uhg", [](const river& r, double dt) { return r.uhg(to_us(dt)); });
+    py::class_<river_network>(m, "RiverNetwork")
+        .def(py::init<>())
+        .def("add", [](river_network& n, const river& r) -> river_network& { return n.add(r); }, py::return_value_policy::reference_internal)
+        .def("remove_by_id", &river_network::remove_by_id)
+        .def("river_by_id", [](river_network& n, int64_t rid) -> river& { return n.river_by_id(rid); }, py::return_value_policy::reference_internal)
+        .def("upstreams_by_id", &river_network::upstreams_by_id)
+        .def("downstream_by_id", &river_network::downstream_by_id)
+        .def("set_downstream_by_id", &river_network::set_downstream_by_id)
+        .def("network_contains_directed_cycle", &river_network::network_contains_directed_cycle);
+    m.def("make_uhg_from_gamma", &make_uhg_from_gamma, py::arg("n_steps"), py::arg("alpha"), py::arg("beta"));
+
+    m.def("utc_time", [](int y, int mo, int d, int h, int mi, int s) { return to_s(utc_time(y, mo, d, h, mi, s)); });
+    m.def("average_values", [](const point_ts& s, const fixed_dt& ta) {
+        auto v = average_values(s, ta);
+        return py::array_t<double>(v.size(), v.data());
+    });
+
+    bind_model<pt_gs_k_stack>(m, "_PTGSKRegionModel");
+    bind_model<hbv_stack_stack>(m, "_HbvRegionModel");
+
+    py::register_exception_translator([](std::exception_ptr p) {
+        try {
+            if (p) std::rethrow_exception(p);
+        } catch (const std::invalid_argument& e) {
+            PyErr_SetString(PyExc_RuntimeError, e.what());
+        }
+    });
+}

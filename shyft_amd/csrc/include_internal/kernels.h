@@ -61,6 +61,10 @@ hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_step
 hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
                                const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream);
 
+// flag = 1 if any of rows x cells (restricted to active cells when active != null) is NaN
+hipError_t launch_nan_scan(const double* f, size_t n_rows, size_t n_cells, const uint8_t* active, int32_t* flag,
+                           hipStream_t stream);
+
 // fill with a constant
 hipError_t launch_fill(double* p, size_t n, double v, hipStream_t stream);
 

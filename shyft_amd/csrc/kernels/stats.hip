@@ -64,6 +64,19 @@ __global__ __launch_bounds__(RB) void segment_sum_kernel(const double* __restric
     if (threadIdx.x == 0) out[c * n_steps + t] = r;
 }
 
+// region_model::is_cell_env_ts_ok (region_model.h:954-962): any NaN in the forcing of a calculated cell.
+// One flag word, set with a plain store by any lane that sees a NaN (all writers store the same value).
+__global__ void nan_scan_kernel(const double* __restrict__ f, size_t n_rows, size_t n_cells,
+                                const uint8_t* __restrict__ active, int32_t* __restrict__ flag) {
+    const size_t total = n_rows * n_cells;
+    bool bad = false;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const double v = f[i];
+        if (v != v && (!active || active[i % n_cells])) bad = true;
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
 __global__ void fill_kernel(double* __restrict__ p, size_t n, double v) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -91,5 +104,15 @@ hipError_t launch_fill(double* p, size_t n, double v, hipStream_t stream) {
     size_t blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(fill_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_nan_scan(const double* f, size_t n_rows, size_t n_cells, const uint8_t* active, int32_t* flag,
+                           hipStream_t stream) {
+    const size_t n = n_rows * n_cells;
+    if (n == 0) return hipSuccess;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(nan_scan_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, f, n_rows, n_cells, active, flag);
     return hipGetLastError();
 }

@@ -331,6 +331,38 @@ std::vector<int32_t> select_cells(const shyft_hip_region* h, const int64_t* ids,
     return sel;
 }
 
+// device rows [step0, step0+n) of a series id (shyft_hip.h: response ids, SHYFT_HIP_SERIES_FORCING + var,
+// SHYFT_HIP_SERIES_STATE + field on the T+1 state axis)
+const double* series_rows(const shyft_hip_region* h, int series, size_t step0, size_t n, const char* what) {
+    const size_t N = h->n;
+    if (series >= SHYFT_HIP_SERIES_STATE) {
+        const int f = series - SHYFT_HIP_SERIES_STATE;
+        if (!h->collect_state || !h->d_state_series.p)
+            throw std::runtime_error(std::string(what) + ": state collection is off");
+        if (f < 0 || size_t(f) >= h->n_state_fields()) throw std::runtime_error(std::string(what) + ": invalid state field");
+        if (step0 < h->w0 || step0 + n > h->w0 + h->TW + 1)
+            throw std::runtime_error(std::string(what) + ": steps outside the resident window");
+        return h->d_state_series.p + (size_t(f) * (h->TW + 1) + (step0 - h->w0)) * N;
+    }
+    check_window(h, step0, n, what);
+    if (series >= SHYFT_HIP_SERIES_FORCING) {
+        const int v = series - SHYFT_HIP_SERIES_FORCING;
+        if (v < 0 || v >= N_FORCING) throw std::runtime_error(std::string(what) + ": invalid forcing variable");
+        return h->d_forcing.p + (size_t(v) * h->TW + (step0 - h->w0)) * N;
+    }
+    if (series < 0 || size_t(series) >= h->n_series())
+        throw std::runtime_error(std::string(what) + ": series not collected in this collection mode");
+    return h->d_resp.p + (size_t(series) * h->TW + (step0 - h->w0)) * N;
+}
+
+template <class T>
+void clone_buf(dbuf<T>& dst, const dbuf<T>& src) {
+    dst.release();
+    if (!src.p) return;
+    dst.alloc(src.n);
+    hip_check(hipMemcpy(dst.p, src.p, src.n * sizeof(T), hipMemcpyDeviceToDevice), "clone");
+}
+
 }  // namespace
 
 extern "C" {
@@ -841,9 +873,7 @@ int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* 
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_statistics: null argument");
     return guarded(h, [&] {
-        if (series < 0 || size_t(series) >= h->n_series())
-            throw std::runtime_error("statistics: series not collected in this collection mode");
-        check_window(h, step0, n, "statistics");
+        const double* src = series_rows(h, series, step0, n, "statistics");
         std::vector<int32_t> sel = select_cells(h, ids, n_ids, scope);
         if (sel.empty()) {  // no match: sum -> empty ts in the reference; average -> nan
             for (size_t t = 0; t < n; ++t) dst[t] = weighted ? NAN : 0.0;
@@ -864,7 +894,6 @@ int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* 
             w = h->d_w.p;
         }
         h->d_tmp.alloc(std::max(h->d_tmp.n, n));
-        const double* src = h->d_resp.p + (size_t(series) * h->TW + (step0 - h->w0)) * h->n;
         hip_check(launch_select_sum(src, h->n, n, h->d_sel.p, sel.size(), w, h->d_tmp.p, h->stream), "select_sum");
         copy_rows(h->stream, dst, h->d_tmp.p, n * sizeof(double), 0, 1);
         if (weighted) {
@@ -879,11 +908,8 @@ int shyft_hip_catchment_sums(const shyft_hip_region* hc, int series, size_t step
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_catchment_sums: null argument");
     return guarded(h, [&] {
-        if (series < 0 || size_t(series) >= h->n_series())
-            throw std::runtime_error("catchment_sums: series not collected in this collection mode");
-        check_window(h, step0, n, "catchment_sums");
+        const double* src = series_rows(h, series, step0, n, "catchment_sums");
         const size_t C = h->cix_to_cid.size();
-        const double* src = h->d_resp.p + (size_t(series) * h->TW + (step0 - h->w0)) * h->n;
         double* out = dst;
         if (!dst_on_device) {
             h->d_tmp.alloc(std::max(h->d_tmp.n, C * n));
@@ -901,6 +927,77 @@ int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids) {
     if (!h || !cids) return fail(const_cast<shyft_hip_region*>(h), "shyft_hip_catchment_ids: null argument");
     for (size_t c = 0; c < h->cix_to_cid.size(); ++c) cids[c] = h->cix_to_cid[c];
     return 0;
+}
+
+int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out) {
+    if (!src || !out) return fail(nullptr, "shyft_hip_region_clone: null argument");
+    *out = nullptr;
+    shyft_hip_region* c = nullptr;
+    if (shyft_hip_region_create(src->stack, src->n, src->device, &c)) return 1;
+    std::unique_ptr<shyft_hip_region, void (*)(shyft_hip_region*)> h(c, shyft_hip_region_destroy);
+    const int rc = guarded(h.get(), [&] {
+        hip_check(hipDeviceSynchronize(), "sync");
+        // host mirrors (every member that is not a device buffer, stream or event)
+        h->err.clear();
+        h->geo = src->geo; h->routing_id = src->routing_id; h->routing_distance = src->routing_distance;
+        h->cid = src->cid; h->cix = src->cix; h->cix_to_cid = src->cix_to_cid; h->cid_to_cix = src->cid_to_cix;
+        h->params = src->params; h->n_sets = src->n_sets; h->set_ix = src->set_ix; h->active = src->active;
+        h->t0 = src->t0; h->dt = src->dt; h->T = src->T; h->w0 = src->w0; h->TW = src->TW;
+        h->collect = src->collect; h->collect_state = src->collect_state;
+        h->derived_dirty = true; h->has_geo = src->has_geo; h->has_params = src->has_params; h->has_state = src->has_state;
+        h->dst_dirty = true;
+        clone_buf(h->d_state, src->d_state);
+        clone_buf(h->d_forcing, src->d_forcing);
+        clone_buf(h->d_resp, src->d_resp);
+        clone_buf(h->d_state_series, src->d_state_series);
+        clone_buf(h->d_doy, src->d_doy);
+        clone_buf(h->d_trel, src->d_trel);
+        clone_buf(h->d_seg_cells, src->d_seg_cells);
+        clone_buf(h->d_seg_off, src->d_seg_off);
+        clone_buf(h->d_active, src->d_active);
+        clone_buf(h->d_alt, src->d_alt);
+    });
+    if (rc) {
+        g_last_error = h->err;
+        return rc;
+    }
+    *out = h.release();
+    return 0;
+}
+
+int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t step0, size_t n, double* buf, int write) {
+    if (!h || !buf) return fail(h, "shyft_hip_cell_series: null argument");
+    return guarded(h, [&] {
+        if (cell >= h->n) throw std::runtime_error("cell_series: cell index out of range");
+        if (write && series < SHYFT_HIP_SERIES_FORCING)
+            throw std::runtime_error("cell_series: only forcing (cell env_ts) is writable");
+        const double* rows = series_rows(h, series, step0, n, "cell_series");
+        double* p = const_cast<double*>(rows) + cell;
+        const size_t pitch = h->n * sizeof(double);
+        if (write)
+            hip_check(hipMemcpy2DAsync(p, pitch, buf, sizeof(double), sizeof(double), n, hipMemcpyHostToDevice, h->stream),
+                      "cell_series write");
+        else
+            hip_check(hipMemcpy2DAsync(buf, sizeof(double), p, pitch, sizeof(double), n, hipMemcpyDeviceToHost, h->stream),
+                      "cell_series read");
+        hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_forcing_ok(const shyft_hip_region* hc, int* ok) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !ok) return fail(h, "shyft_hip_forcing_ok: null argument");
+    return guarded(h, [&] {
+        *ok = 0;
+        if (h->T == 0) throw std::runtime_error("is_cell_env_ts_ok: no time axis (initialize_cell_environment)");
+        hip_check(hipMemsetAsync(h->d_flag.p, 0, sizeof(int32_t), h->stream), "memset");
+        const uint8_t* active = h->active.empty() ? nullptr : h->d_active.p;
+        hip_check(launch_nan_scan(h->d_forcing.p, N_FORCING * h->TW, h->n, active, h->d_flag.p, h->stream), "nan_scan");
+        int32_t flag = 0;
+        hip_check(hipMemcpyAsync(&flag, h->d_flag.p, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), "download");
+        hip_check(hipStreamSynchronize(h->stream), "sync");
+        *ok = flag ? 0 : 1;
+    });
 }
 
 }  // extern "C"

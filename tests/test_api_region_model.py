@@ -1,0 +1,229 @@
+"""The reference's Python region-model scenario run through shyft_amd.api on the GPU.
+
+Follows shyft/tests/api/test_region_model_stacks.py:14-30 (build_model), :46-55
+(create_dummy_region_environment), :91-112 (area statistics), :114-310
+(test_model_initialize_and_run: interpolation, is_cell_env_ts_ok, set_states,
+state collection, run_cells, the statistics KATs -110.6998 / -16.7138 / 107.3981 /
+0.189214067680088 / 0.9995599424191931, opt-model clone, stepwise 10 x 24 runs,
+illegal cids, rasters, river network out(8) = 28.06, adjust_q) and :424-479 (hbv).
+The KAT values are the reference's own; everything here goes through the C++ host
+class and the C ABI (no oracle involved).
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def build_model(model_t, parameter_t, n, num_catchments=1):
+    from shyft_amd import api
+    gcds = api.GeoCellDataVector()
+    for i in range(n):
+        gp = api.GeoPoint(500 + 1000.0 * i, 500.0, 500.0 * i / n)
+        ltf = api.LandTypeFractions(0.01, 0.05, 0.19, 0.3, 0.45)
+        g = api.GeoCellData(gp, 1000 * 1000, 1 if num_catchments == 1 else 1 + i % num_catchments, 0.9, ltf)
+        g.land_type_fractions_info().set_fractions(glacier=0.01, lake=0.05, reservoir=0.19, forest=0.3)
+        gcds.append(g)
+    return model_t(gcds, parameter_t())
+
+
+def constant_source(src_t, gp, period, value):
+    from shyft_amd import api
+    tv = api.UtcTimeVector([period.start])
+    vv = api.DoubleVector([value])
+    return src_t(gp, api.TsFactory().create_time_point_ts(period, tv, vv, api.POINT_AVERAGE_VALUE))
+
+
+def dummy_env(ta, gp):
+    from shyft_amd import api
+    p = api.UtcPeriod(*ta.total_period())
+    re = api.ARegionEnvironment()
+    re.precipitation.append(constant_source(api.PrecipitationSource, gp, p, 5.0))
+    re.temperature.append(constant_source(api.TemperatureSource, gp, p, 10.0))
+    re.wind_speed.append(constant_source(api.WindSpeedSource, gp, p, 2.0))
+    re.rel_hum.append(constant_source(api.RelHumSource, gp, p, 0.7))
+    re.radiation = api.RadiationSourceVector()
+    re.radiation.append(constant_source(api.RadiationSource, gp, p, 300.0))
+    return re
+
+
+def interpolation_parameter():
+    from shyft_amd import api
+    ip = api.InterpolationParameter()
+    ip.temperature_idw.default_temp_gradient = -0.005
+    ip.temperature_idw.gradient_by_equation = True
+    ip.temperature_idw.max_members = 6
+    ip.temperature_idw.max_distance = 20000
+    assert ip.temperature_idw.zscale == pytest.approx(1.0)
+    ip.temperature_idw.zscale = 0.5
+    ip.temperature_idw.distance_measure_factor = 1.0
+    ip.use_idw_for_temperature = True
+    assert ip.precipitation.scale_factor == pytest.approx(1.02)
+    return ip
+
+
+def test_model_area_functions():
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k
+    m = build_model(pt_gs_k.PTGSKModel, pt_gs_k.PTGSKParameter, 20)
+    cids = api.IntVector()
+    st = m.statistics
+    total = st.total_area(cids)
+    assert st.snow_storage_area(cids) == pytest.approx(total - st.lake_area(cids) - st.reservoir_area(cids))
+    assert total == pytest.approx(st.forest_area(cids) + st.glacier_area(cids) + st.lake_area(cids) +
+                                  st.reservoir_area(cids) + st.unspecified_area(cids))
+    assert abs(st.elevation(cids) - 475 / 2.0) < 1e-3
+    cids.append(3)
+    with pytest.raises(RuntimeError):
+        st.total_area(cids)
+
+
+def test_model_initialize_and_run():
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k
+    n = 20
+    model = build_model(pt_gs_k.PTGSKModel, pt_gs_k.PTGSKParameter, n)
+    assert model.size() == n
+    assert model.ncore >= 1
+    model.ncore = 4
+    assert model.ncore == 4
+    rp = model.get_region_parameter()
+    rp.gs.snow_cv_forest_factor = 0.1
+    rp.gs.snow_cv_altitude_factor = 0.0001
+    assert rp.gs.effective_snow_cv(1.0, 0.0) == pytest.approx(rp.gs.snow_cv + 0.1)
+    assert rp.gs.effective_snow_cv(1.0, 1000.0) == pytest.approx(rp.gs.snow_cv + 0.1 + 0.1)
+    cal = api.Calendar()
+    ta = api.TimeAxisFixedDeltaT(cal.time(2015, 1, 1, 0, 0, 0), api.deltahours(1), 240)
+    ip = interpolation_parameter()
+    model.initialize_cell_environment(ta)
+    model.interpolate(ip, dummy_env(ta, model.get_cells()[n // 2].geo.mid_point()))
+    assert model.interpolation_parameter.use_idw_for_temperature
+    assert model.interpolation_parameter.temperature_idw.zscale == pytest.approx(0.5)
+    c0 = model.cells[0]
+    for x in (c0.env_ts.temperature, c0.env_ts.precipitation, c0.env_ts.rel_hum, c0.env_ts.radiation,
+              c0.env_ts.wind_speed):
+        assert model.is_cell_env_ts_ok()
+        vx = x.value(0)
+        x.set(0, float("nan"))
+        assert not model.is_cell_env_ts_ok()
+        x.set(0, vx)
+        assert model.is_cell_env_ts_ok()
+
+    s0 = pt_gs_k.PTGSKStateVector()
+    for _ in range(n):
+        si = pt_gs_k.PTGSKState()
+        si.kirchner.q = 40.0
+        s0.append(si)
+    model.set_states(s0)
+    model.set_state_collection(-1, True)
+    model2 = pt_gs_k.PTGSKModel(model)
+    opt_model = pt_gs_k.create_opt_model_clone(model)
+    model.run_cells()
+    cids = api.IntVector()
+    sum_discharge = model.statistics.discharge(cids)
+    sum_discharge_value = model.statistics.discharge_value(cids, 0)
+    assert model.statistics.charge_value(cids, 0) == pytest.approx(-110.6998, abs=0.5e-2)
+    cell_charge = model.statistics.charge_value(api.IntVector([0, 1, 3]), 0, ix_type=api.stat_scope.cell)
+    assert cell_charge == pytest.approx(-16.7138, abs=0.5e-2)
+    s126 = model.statistics.charge(api.IntVector([1, 2, 6]), ix_type=api.stat_scope.cell).values.to_numpy().sum()
+    assert s126 == pytest.approx(107.3981, abs=0.5e-2)
+    ae_output = model.actual_evaptranspiration_response.output(cids)
+    ae_pot_ratio = model.actual_evaptranspiration_response.pot_ratio(cids)
+    assert ae_output.values.to_numpy().max() == pytest.approx(0.189214067680088, abs=0.5e-7)
+    assert ae_pot_ratio.values.to_numpy().min() == pytest.approx(0.9995599424191931, abs=0.5e-7)
+    assert ae_pot_ratio.values.to_numpy().max() == pytest.approx(1.0, abs=0.5e-7)
+    opt_model.run_cells()
+    assert opt_model.statistics.discharge_value(cids, 0) == pytest.approx(sum_discharge_value, abs=0.5e-3)
+    assert sum_discharge_value >= 130.0
+    # the reference asserts the clone SHARES the region env (apoint_ts shared impl): a set on one shows on the other
+    opt_model.region_env.temperature[0].ts.set(0, 23.2)
+    assert not abs(model.region_env.temperature[0].ts.value(0) - opt_model.region_env.temperature[0].ts.value(0)) > 0.5
+
+    # stepwise 10 x 24 runs equal the full run
+    model.set_states(s0)
+    assert len(s0) == len(model.initial_state)
+    for collect in (False, True):
+        model2.set_state_collection(-1, collect)
+        model2.set_states(s0)
+        for section in range(10):
+            model2.run_cells(use_ncore=0, start_step=section * 24, n_steps=24)
+            assert model2.statistics.discharge(cids).size() == sum_discharge.size()
+    diff = sum_discharge.values.to_numpy() - model2.statistics.discharge(cids).values.to_numpy()
+    assert (diff * diff).max() == pytest.approx(0.0, abs=0.5e-4)
+    with pytest.raises(RuntimeError):
+        model.statistics.discharge(api.IntVector([0, 4, 5]))
+
+    assert model.statistics.temperature(cids).size() == ta.size()
+    assert model.statistics.precipitation(cids) is not None
+    for t in range(ta.size()):
+        assert len(model.statistics.precipitation(cids, t)) == n
+    assert model.gamma_snow_response.sca_value(cids, 1) >= 0.0
+    assert model.gamma_snow_response.sca(cids) is not None
+    assert model.gamma_snow_state.albedo(cids) is not None
+    copy_model = model.__class__(model)
+    copy_model.run_cells()
+
+    # routing: one river 3000 m downstream at 1/3.6 m/s, UHG alpha 7 (test_region_model_stacks.py:287-301)
+    model.river_network.add(api.River(1, api.RoutingInfo(0, 3000.0), api.UHGParameter(1 / 3.60, 7.0, 0.0)))
+    model.connect_catchment_to_river(1, 1)
+    assert model.has_routing()
+    out = model.river_output_flow_m3s(1)
+    local = model.river_local_inflow_m3s(1)
+    up = model.river_upstream_inflow_m3s(1)
+    assert out.value(8) == pytest.approx(28.061248025828114, abs=0.5)
+    # no cell UHG (routing distance 0): local inflow equals the cells' summed discharge; no upstream rivers
+    assert np.allclose(local.values.to_numpy(), sum_discharge.values.to_numpy(), rtol=1e-12, atol=1e-12)
+    assert np.all(up.values.to_numpy() == 0.0)
+    model.connect_catchment_to_river(1, 0)
+    assert not model.has_routing()
+
+    q_0 = model.cells[0].state.kirchner.q
+    model.adjust_q(2.0, cids)
+    assert model.cells[0].state.kirchner.q == pytest.approx(q_0 * 2.0)
+    model.revert_to_initial_state()
+    model.run_cells(0, 10, 2)
+
+
+def test_run_cells_argument_errors():
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k
+    m = build_model(pt_gs_k.PTGSKOptModel, pt_gs_k.PTGSKParameter, 4)
+    with pytest.raises(RuntimeError, match="invalid time_axis"):
+        m.run_cells()
+    ta = api.TimeAxisFixedDeltaT(api.Calendar().time(2015, 1, 1), api.deltahours(1), 24)
+    m.initialize_cell_environment(ta)
+    with pytest.raises(RuntimeError, match="start_step must in range"):
+        m.run_cells(0, 24, 0)
+    with pytest.raises(RuntimeError, match="start_step\\+n_steps must be within"):
+        m.run_cells(0, 10, 20)
+    with pytest.raises(RuntimeError, match="more than 100 time"):
+        m.run_cells(1000 * m.ncore)
+    with pytest.raises(RuntimeError):
+        m.set_catchment_calculation_filter(api.IntVector([7]))
+
+
+def test_hbv_model_discharge():
+    """test_region_model_stacks.py:424-479: hbv_stack, tank uz = lz = 40, discharge_value(0) >= 32."""
+    from shyft_amd import api
+    from shyft_amd.api import hbv_stack
+    n = 20
+    model = build_model(hbv_stack.HbvModel, hbv_stack.HbvParameter, n)
+    cal = api.Calendar()
+    ta = api.TimeAxisFixedDeltaT(cal.time(2015, 1, 1, 0, 0, 0), api.deltahours(1), 240)
+    model.initialize_cell_environment(ta)
+    model.interpolate(interpolation_parameter(), dummy_env(ta, model.get_cells()[n // 2].geo.mid_point()))
+    s0 = hbv_stack.HbvStateVector()
+    for _ in range(n):
+        si = hbv_stack.HbvState()
+        si.tank.uz = 40.0
+        si.tank.lz = 40.0
+        s0.append(si)
+    model.set_states(s0)
+    model.set_state_collection(-1, True)
+    model.run_cells()
+    cids = api.IntVector()
+    assert model.statistics.discharge_value(cids, 0) >= 32.0
+    assert model.hbv_snow_state.swe(cids).size() == ta.size() + 1
+    assert math.isfinite(model.hbv_tank_state.uz_value(cids, 10))

@@ -1,0 +1,100 @@
+"""CPU checks of the host layer's data types (no device calls): the pybind11 module loads,
+parameter/state objects keep the reference's get/set order and names, source resampling
+(average_accessor) and the routing UHG / river network follow the reference."""
+import math
+
+import numpy as np
+import pytest
+
+from shyft_amd import api
+from shyft_amd.api import hbv_stack, pt_gs_k
+
+HOUR = 3600
+
+
+def test_parameter_order_and_names():
+    p = pt_gs_k.PTGSKParameter()
+    assert p.size() == 31
+    assert p.get_name(0) == "kirchner.c1" and p.get_name(30) == "msp.reservoir_direct_response_fraction"
+    p.gs.snow_cv = 0.5
+    assert p.get(14) == 0.5
+    v = list(range(31))
+    p.set(v)
+    assert p.kirchner.c3 == 2 and p.gs.n_winter_days == 28
+    with pytest.raises(RuntimeError, match="PTGSK Parameter Accessor: .set size missmatch"):
+        p.set(v[:30])
+    h = hbv_stack.HbvParameter()
+    assert h.size() == 22 and h.get_name(8) == "hs.lw"
+    assert len(h.to_vector()) == 22 + 17
+
+
+def test_hbv_snow_distribution_normalisation():
+    """normalize_snow_distribution (hbv_snow.h:63-66) with the trapezoid of hbv_snow_common.h:14-40."""
+    h = hbv_stack.HbvParameter()
+    h.snow_s = [1.0, 2.0, 3.0]
+    h.snow_intervals = [0.0, 0.5, 1.0]
+    v = h.to_vector()
+    area = 0.5 * (1 + 2) * 0.5 + 0.5 * (2 + 3) * 0.5
+    assert v[22] == 3.0
+    assert np.allclose(v[23:26], np.array([1, 2, 3]) / area)
+
+
+def test_average_accessor_stair_case_and_linear():
+    """average_value over [t, t+dt) of a point series (time_series.h:202-310)."""
+    t0 = api.Calendar().time(2015, 1, 1)
+    ta = api.TimeAxisFixedDeltaT(t0, HOUR, 4)
+    # stair case: points every 2 h
+    src = api.TsFactory().create_time_point_ts(api.UtcPeriod(t0, t0 + 4 * HOUR), [t0, t0 + 2 * HOUR], [1.0, 3.0],
+                                               api.POINT_AVERAGE_VALUE)
+    assert list(src.average(ta).values) == [1.0, 1.0, 3.0, 3.0]
+    # linear between points: mean of the line over each hour; the last point is not extended (strict)
+    lin = api.TsFactory().create_time_point_ts(api.UtcPeriod(t0, t0 + 4 * HOUR), [t0, t0 + 2 * HOUR], [1.0, 3.0],
+                                               api.POINT_INSTANT_VALUE)
+    v = lin.average(ta).values
+    assert v[0] == pytest.approx(1.5) and v[1] == pytest.approx(2.5)
+    assert math.isnan(v[2]) and math.isnan(v[3])
+    # NaN beyond the source end (USE_NAN extension)
+    short = api.TsFactory().create_time_point_ts(api.UtcPeriod(t0, t0 + HOUR), [t0], [7.0], api.POINT_AVERAGE_VALUE)
+    v = short.average(ta).values
+    assert v[0] == 7.0 and all(math.isnan(x) for x in v[1:])
+
+
+def test_uhg_matches_scipy_gamma():
+    """make_uhg_from_gamma (routing.h:399-421): pdf(Gamma(alpha,1), i*q99/n) + beta, normalised."""
+    ss = pytest.importorskip("scipy.stats")
+    for n, alpha, beta in [(3, 7.0, 0.0), (10, 3.0, 0.0), (24, 7.0, 0.01), (5, 1.5, -0.01)]:
+        w = np.array(api.make_uhg_from_gamma(n, alpha, beta))
+        x = np.arange(n) * ss.gamma(alpha).ppf(0.99) / n
+        y = np.maximum(0.0, ss.gamma(alpha).pdf(x) + beta)
+        assert np.allclose(w, y / y.sum(), rtol=1e-12, atol=1e-15)
+    assert api.make_uhg_from_gamma(1, 7.0, 0.0) == [1.0]
+    assert api.make_uhg_from_gamma(0, 7.0, 0.0) == [1.0]
+
+
+def test_river_network_rules():
+    """river_network::add / cycle checks (routing.h:140-233)."""
+    rn = api.RiverNetwork()
+    rn.add(api.River(1))
+    rn.add(api.River(2, api.RoutingInfo(1, 1000.0)))
+    rn.add(api.River(3, api.RoutingInfo(2, 500.0)))
+    assert rn.upstreams_by_id(1) == [2]
+    assert rn.downstream_by_id(3) == 2
+    with pytest.raises(RuntimeError, match="already registered"):
+        rn.add(api.River(2))
+    with pytest.raises(RuntimeError, match="does not yet exist"):
+        rn.add(api.River(9, api.RoutingInfo(8, 1.0)))
+    with pytest.raises(RuntimeError, match="cycle"):
+        rn.set_downstream_by_id(1, 3)
+    with pytest.raises(RuntimeError, match="must be >0"):
+        rn.add(api.River(0))
+    # river UHG length: round(distance / velocity / dt)
+    r = api.River(5, api.RoutingInfo(1, 3000.0), api.UHGParameter(1 / 3.6, 7.0, 0.0))
+    assert len(r.uhg(HOUR)) == 3
+
+
+def test_land_type_fractions_validation():
+    f = api.LandTypeFractions()
+    with pytest.raises(RuntimeError):
+        f.set_fractions(glacier=0.5, lake=0.5, reservoir=0.5, forest=0.0)
+    f.set_fractions(glacier=0.2, lake=0.2, reservoir=0.2, forest=0.4004)  # within 1e-3: normalised
+    assert f.glacier() + f.lake() + f.reservoir() + f.forest() == pytest.approx(1.0)
