@@ -145,6 +145,86 @@ int oracle_ptgsk_run(size_t n_cells, const double* geo11, const double* params, 
     return 0;
 }
 
+// ---------------------------------------------------------------- pt_ss_k / skaugen
+// skaugen::calculator::step on one state: st = nu alpha sca swe free_water residual num_units (7 doubles),
+// p8 = alpha_0 d_range unit_size max_water_fraction tx cx ts cfr; resp = outflow sca swe. Returns 1 on a throw.
+int oracle_skaugen_step(double* st, double* resp, int64_t dt_us, const double* p8, double T, double prec_mm_h) {
+    skaugen::parameter p{p8[0], p8[1], p8[2], p8[3], p8[4], p8[5], p8[6], p8[7]};
+    skaugen::state s;
+    s.nu = st[0]; s.alpha = st[1]; s.sca = st[2]; s.swe = st[3]; s.free_water = st[4]; s.residual = st[5];
+    s.num_units = size_t(st[6]);
+    skaugen::response r;
+    try {
+        skaugen::step(dt_us, p, T, prec_mm_h, s, r);
+    } catch (...) {
+        return 1;
+    }
+    st[0] = s.nu; st[1] = s.alpha; st[2] = s.sca; st[3] = s.swe; st[4] = s.free_water; st[5] = s.residual;
+    st[6] = double(s.num_units);
+    resp[0] = r.outflow; resp[1] = r.sca; resp[2] = r.swe;
+    return 0;
+}
+
+double oracle_skaugen_sca_rel_red(uint64_t u, uint64_t n, double nu_a, double alpha) {
+    return skaugen::statistics::sca_rel_red(u, n, 0.0, nu_a, alpha);
+}
+
+// Run the pt_ss_k region model on the CPU with the reference scheduler.
+//  params : n_sets x 21 (pt_ss_k.h:78-101 order); state : n_cells x 8 in/out
+//  out_main : [2][T][N]; out_full : [8][T][N] (series-id order); out_state : [7][T+1][N]
+int oracle_ptssk_run(size_t n_cells, const double* geo11, const double* params, size_t n_sets, const int32_t* set_ix,
+                     double* state, int64_t t0_us, int64_t dt_us, size_t T, int start_step, int n_steps, const double* temp,
+                     const double* prec, const double* ws, const double* rh, const double* rad, double* out_main,
+                     double* out_full, double* out_state, int ncore, double* elapsed_s, char* err, size_t errlen) {
+    try {
+        ptssk_region rm;
+        rm.time_axis = fixed_dt(t0_us, dt_us, T);
+        rm.params.resize(n_sets);
+        for (size_t k = 0; k < n_sets; ++k) rm.params[k].set(params + k * pt_ss_k::parameter::size());
+        rm.cells.resize(n_cells);
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.geo = geo_cell_data::from_raw(geo11 + i * 11);
+            int32_t k = set_ix ? set_ix[i] : 0;
+            if (k < 0 || size_t(k) >= n_sets) return fail(err, errlen, "oracle_ptssk_run: parameter set index out of range");
+            c.parameter = &rm.params[k];
+            c.state.set(state + i * pt_ss_k::state::size());
+            c.temp.resize(T); c.prec.resize(T); c.ws.resize(T); c.rh.resize(T); c.rad.resize(T);
+            for (size_t t = 0; t < T; ++t) {
+                c.temp[t] = temp[t * n_cells + i];
+                c.prec[t] = prec[t * n_cells + i];
+                c.ws[t] = ws[t * n_cells + i];
+                c.rh[t] = rh[t * n_cells + i];
+                c.rad[t] = rad[t * n_cells + i];
+            }
+            c.col.full = out_full != nullptr;
+            c.col.collect_state = out_state != nullptr;
+        }
+        auto t_begin = std::chrono::steady_clock::now();
+        rm.run_cells(size_t(ncore < 0 ? 0 : ncore), start_step, n_steps);
+        auto t_end = std::chrono::steady_clock::now();
+        if (elapsed_s) *elapsed_s = std::chrono::duration<double>(t_end - t_begin).count();
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.state.get(state + i * pt_ss_k::state::size());
+            for (size_t t = 0; t < T; ++t) {
+                if (out_main) {
+                    out_main[t * n_cells + i] = c.col.rc[pt_ss_k::AVG_DISCHARGE][t];
+                    out_main[(T + t) * n_cells + i] = c.col.rc[pt_ss_k::CHARGE_M3S][t];
+                }
+                if (out_full)
+                    for (int k = 0; k < pt_ss_k::N_ALL; ++k) out_full[(size_t(k) * T + t) * n_cells + i] = c.col.rc[k][t];
+            }
+            if (out_state)
+                for (int k = 0; k < pt_ss_k::N_SC; ++k)
+                    for (size_t t = 0; t <= T; ++t) out_state[(size_t(k) * (T + 1) + t) * n_cells + i] = c.col.sc[k][t];
+        }
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
 }  // extern "C"
 
 // Inverse-distance interpolation of one variable (kind: 0 temperature, 1 precipitation,

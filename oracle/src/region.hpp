@@ -13,6 +13,7 @@
 #include "common.hpp"
 #include "hbv.hpp"
 #include "ptgsk.hpp"
+#include "ptssk.hpp"
 
 namespace oracle {
 
@@ -45,6 +46,21 @@ struct hbv_cell {
         col.initialize(ta.size(), start_step, n_steps, geo.area);
         pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
         hbv_stack::run_hbv_stack(geo, *parameter, ta, start_step, n_steps, fv, state, col);
+    }
+};
+
+// pt_ss_k cell (pt_ss_k_cell_model.h:205-256)
+struct ptssk_cell {
+    geo_cell_data geo;
+    const pt_ss_k::parameter* parameter = nullptr;
+    pt_ss_k::state state;
+    std::vector<double> temp, prec, ws, rh, rad;
+    pt_ss_k::collectors col;
+    void run(const fixed_dt& ta, int start_step, int n_steps) {
+        if (parameter == nullptr) throw std::runtime_error("pt_ss_k::run with null parameter attempted");
+        col.initialize(ta.size(), start_step, n_steps, geo.area);
+        pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
+        pt_ss_k::run_pt_ss_k(geo, *parameter, ta, start_step, n_steps, fv, state, col);
     }
 };
 
@@ -110,5 +126,6 @@ struct region_of {
 
 using ptgsk_region = region_of<ptgsk_cell, pt_gs_k::parameter>;
 using hbv_region = region_of<hbv_cell, hbv_stack::parameter>;
+using ptssk_region = region_of<ptssk_cell, pt_ss_k::parameter>;
 
 }  // namespace oracle

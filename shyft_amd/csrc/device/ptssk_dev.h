@@ -1,0 +1,325 @@
+// Skaugen snow (core/skaugen.h:43-380) for the pt_ss_k kernel (gfx950, fp64).
+//
+// Lane = cell; the whole snow state lives in registers. Unit counts are
+// unsigned 64-bit like the reference's unsigned long (including its wrap-around
+// on a negative lrint), lrint rounds half to even (v_rndne_f64).
+//
+// The expensive part is statistics::sca_rel_red (skaugen.h:57-82), evaluated
+// only on a partial melt of a snowpack: a 2-bit Brent minimisation of
+// pdf_m - pdf_a, a walk of the lower bracket, a 10-bit bisection and two gamma
+// cdfs. The gamma distribution functions are boost's full-precision ones
+// restated on detmath (pdf = prefix/z/theta, cdf = P(k, z)), the same
+// expressions the CPU oracle evaluates (oracle/src/ptssk.hpp), so the kernel is
+// bit-identical to it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "special.h"
+
+namespace shyft_dev {
+
+struct ss_par {
+    double alpha_0, d_range, unit_size, max_water_fraction, tx, cx, ts, cfr;
+};
+
+struct ss_state {
+    double nu, alpha, sca, swe, free_water, residual;
+    uint64_t num_units;
+};
+
+__device__ inline long ss_lrint(double x) { return (long)rint(x); }
+
+// gamma_distribution(k, theta) pdf with boost's pole/zero handling at x = 0; err set on the pole
+__device__ inline double ss_gamma_pdf(double k, double theta, double lgk, double x, int32_t& err) {
+    if (x == 0) {
+        if (k == 1) return 1 / theta;
+        if (k < 1) {
+            err = ERR_SKAUGEN_PDF;
+            return 0.0;
+        }
+        return 0.0;
+    }
+    const double z = x / theta;
+    const double prefix = dexp(k * dlog(z) - z - lgk);
+    return prefix / z / theta;
+}
+
+__device__ inline double ss_c(uint64_t n, double d_range) { return dexp(-(double)n / d_range); }
+
+// statistics::sca_rel_red (skaugen.h:57-82)
+__device__ __noinline__ double ss_sca_rel_red(uint64_t u, uint64_t n, double nu_a, double alpha, int32_t& err) {
+    const double nu_m = ((double)u / n) * nu_a;
+    const double theta = 1.0 / alpha;
+    const double lg_m = dlgamma(nu_m), lg_a = dlgamma(nu_a);
+    const double g_a_mean = nu_a * theta;
+    auto zero_func = [&](double x) { return ss_gamma_pdf(nu_m, theta, lg_m, x, err) - ss_gamma_pdf(nu_a, theta, lg_a, x, err); };
+    double lower = nu_m * theta;
+    double upper;
+    {  // brent_find_minima(zero_func, 0, g_a_mean, 2 bits), boost tools/minima.hpp
+        double min = 0.0, max = g_a_mean;
+        const double tolerance = 0.5;  // ldexp(1, 1-2)
+        const double golden = (double)0.3819660f;
+        double x, w, v, uu, delta, delta2, fu, fv, fw, fx, mid, fract1, fract2;
+        x = w = v = max;
+        fw = fv = fx = zero_func(x);
+        delta2 = delta = 0;
+        uint64_t count = ~uint64_t(0);
+        do {
+            mid = (min + max) / 2;
+            fract1 = tolerance * fabs(x) + tolerance / 4;
+            fract2 = 2 * fract1;
+            if (fabs(x - mid) <= (fract2 - (max - min) / 2)) break;
+            if (fabs(delta2) > fract1) {
+                double r = (x - w) * (fx - fv);
+                double q = (x - v) * (fx - fw);
+                double p = (x - v) * q - (x - w) * r;
+                q = 2 * (q - r);
+                if (q > 0) p = -p;
+                q = fabs(q);
+                double td = delta2;
+                delta2 = delta;
+                if ((fabs(p) >= fabs(q * td / 2)) || (p <= q * (min - x)) || (p >= q * (max - x))) {
+                    delta2 = (x >= mid) ? min - x : max - x;
+                    delta = golden * delta2;
+                } else {
+                    delta = p / q;
+                    uu = x + delta;
+                    if (((uu - min) < fract2) || ((max - uu) < fract2)) delta = (mid - x) < 0 ? -fabs(fract1) : fabs(fract1);
+                }
+            } else {
+                delta2 = (x >= mid) ? min - x : max - x;
+                delta = golden * delta2;
+            }
+            uu = (fabs(delta) >= fract1) ? (x + delta) : (delta > 0 ? x + fabs(fract1) : x - fabs(fract1));
+            fu = zero_func(uu);
+            if (fu <= fx) {
+                if (uu >= x) min = x; else max = x;
+                v = w; w = x; x = uu;
+                fv = fw; fw = fx; fx = fu;
+            } else {
+                if (uu < x) min = uu; else max = uu;
+                if ((fu <= fw) || (w == x)) {
+                    v = w; w = uu; fv = fw; fw = fu;
+                } else if ((fu <= fv) || (v == x) || (v == w)) {
+                    v = uu; fv = fu;
+                }
+            }
+        } while (--count);
+        upper = x;
+    }
+    // while (pdf(g_m, lower) < pdf(g_a, lower)) lower *= 0.9; -- 0.9^k underflows to 0 within 7100 steps
+    for (int it = 0; it < 8000 && ss_gamma_pdf(nu_m, theta, lg_m, lower, err) < ss_gamma_pdf(nu_a, theta, lg_a, lower, err);
+         ++it)
+        lower *= 0.9;
+    // bisect(zero_func, lower, upper, eps_tolerance(10), max_iter = 100), boost tools/roots.hpp
+    double bmin = lower, bmax = upper;
+    {
+        double fmin = zero_func(bmin);
+        double fmax = zero_func(bmax);
+        if (fmin == 0) {
+            bmax = bmin;
+        } else if (fmax == 0) {
+            bmin = bmax;
+        } else if (bmin >= bmax || fmin * fmax >= 0) {
+            err = ERR_SKAUGEN_BISECT;  // boost raises evaluation_error
+        } else {
+            const double eps = 0x1p-9;  // max(ldexp(1, 1-10), 4*DBL_EPSILON)
+            int count = 97;             // max_iter 100 minus the three evaluations so far
+            while (count && !(fabs(bmin - bmax) <= eps * smin(fabs(bmin), fabs(bmax)))) {
+                const double mid = (bmin + bmax) / 2;
+                const double fmid = zero_func(mid);
+                if ((mid == bmax) || (mid == bmin)) break;
+                if (fmid == 0) {
+                    bmin = bmax = mid;
+                    break;
+                }
+                const int sm = fmid > 0 ? 1 : (fmid < 0 ? -1 : 0), sn = fmin > 0 ? 1 : (fmin < 0 ? -1 : 0);
+                if (sm * sn < 0) {
+                    bmax = mid;
+                    fmax = fmid;
+                } else {
+                    bmin = mid;
+                    fmin = fmid;
+                }
+                --count;
+            }
+        }
+    }
+    const double x = (bmin + bmax) * 0.5;
+    const double m = gamma_p_prefix(nu_m, x / theta, lg_m, 2.220446049250313e-16).p;
+    const double a = gamma_p_prefix(nu_a, x / theta, lg_a, 2.220446049250313e-16).p;
+    return a + 1.0 - m;
+}
+
+// calculator::compute_shape_vars (skaugen.h:338-380)
+__device__ inline void ss_compute_shape_vars(const ss_par& p, uint64_t nnn, uint64_t n, uint64_t u, double sca,
+                                             double rel_red_sca, double& alpha, double& nu) {
+    const double alpha_0 = p.alpha_0;
+    const double nu_0 = p.alpha_0 * p.unit_size;
+    const double dyn_var = nu / (alpha * alpha);
+    const double init_var = nu_0 / (alpha_0 * alpha_0);
+    double tot_var = 0.0;
+    double tot_mean = 0.0;
+    if (n > 0) {
+        if (nnn == 0) {
+            tot_var = (double)n * init_var * (1 + (double)(n - 1) * ss_c(n, p.d_range));
+            tot_mean = (double)n * nu_0 / alpha_0;
+        } else {
+            const double old_var_cov =
+                (double)(nnn + n) * init_var * (1 + (double)((nnn + n) - 1) * ss_c(nnn + n, p.d_range));
+            const double new_var_cov = (double)n * init_var * (1 + (double)(n - 1) * ss_c(n, p.d_range));
+            tot_var = old_var_cov * sca * sca + new_var_cov * (1.0 - sca) * (1.0 - sca);
+            tot_mean = (sca * (double)(nnn + n) + (1.0 - sca) * (double)n) * p.unit_size;
+        }
+    }
+    if (u > 0) {
+        const double factor =
+            (dyn_var / ((double)nnn * init_var) + 1.0 + (double)(nnn - 1) * ss_c(nnn, p.d_range)) / (double)(2 * nnn);
+        const double non_cond_mean = (double)(nnn - u) * p.unit_size;
+        tot_mean = non_cond_mean / (1.0 - rel_red_sca);
+        const uint64_t cond_u = (uint64_t)ss_lrint((1.0 - rel_red_sca) * (double)nnn - (double)(nnn - u));
+        const double auto_var =
+            cond_u > 0 ? init_var * (double)cond_u * (1.0 + ((double)cond_u - 1.0) * ss_c(cond_u, p.d_range)) : 0.0;
+        const double cross_var = cond_u > 0 ? init_var * (double)cond_u * 2.0 * factor * (double)cond_u : 0.0;
+        tot_var = dyn_var + auto_var - cross_var;
+    }
+    if (fabs(tot_mean) < 1.0e-7) {
+        nu = nu_0;
+        alpha = alpha_0;
+        return;
+    }
+    nu = tot_mean * tot_mean / tot_var;
+    alpha = nu / (p.unit_size * (double)ss_lrint(tot_mean / p.unit_size));
+}
+
+// calculator::step (skaugen.h:151-336); returns the response (outflow, sca, swe) through r_*
+__device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_hours, double T, double prec_mm_h,
+                               ss_state& s, double& r_outflow, double& r_sca, double& r_swe, int32_t& err) {
+    const double snow_tol = 1.0e-10;
+    const double unit_size = p.unit_size;
+    const double prec = prec_mm_h * dt_hours;
+    const double corr_prec = smax(0.0, prec + s.residual);
+    s.residual = smin(0.0, prec + s.residual);
+    const double snow = T < p.tx ? corr_prec : 0.0;
+    const double rain = T < p.tx ? 0.0 : corr_prec;
+
+    if (s.sca * s.swe < unit_size && snow < snow_tol) {
+        r_outflow = (rain + s.sca * (s.swe + s.free_water) + s.residual) / dt_hours;
+        s.residual = 0.0;
+        if (r_outflow < 0.0) {
+            s.residual = r_outflow;
+            r_outflow = 0.0;
+        }
+        s.nu = p.alpha_0 * unit_size;
+        s.alpha = p.alpha_0;
+        s.sca = 0.0;
+        s.swe = 0.0;
+        s.free_water = 0.0;
+        s.num_units = 0;
+        r_sca = 0.0;
+        r_swe = 0.0;
+        return;
+    }
+
+    const double alpha_0 = p.alpha_0;
+    double swe = s.swe;
+    uint64_t nnn = s.num_units;
+    double sca = s.sca;
+    double nu = s.nu;
+    double alpha = s.alpha;
+    if (nnn > 0) {
+        nu *= (double)nnn;
+    } else {
+        nu = alpha_0 * p.unit_size;
+        alpha = alpha_0;
+    }
+
+    double total_new_snow = snow;
+    double lwc = s.free_water;
+    const double total_storage = swe + lwc;
+    double pot_melt = p.cx * step_in_days * (T - p.ts);
+    const double refreeze = smin(smax(0.0, -pot_melt * p.cfr), lwc);
+    total_new_snow += sca * refreeze;
+    lwc -= refreeze;
+    pot_melt = smax(0.0, pot_melt);
+    const double new_snow_reduction = smin(pot_melt, total_new_snow);
+    pot_melt -= new_snow_reduction;
+    total_new_snow -= new_snow_reduction;
+
+    uint64_t n = 0;
+    if (total_new_snow > unit_size) {  // 1. accumulation
+        n = (uint64_t)ss_lrint(total_new_snow / unit_size);
+        ss_compute_shape_vars(p, nnn, n, 0, sca, 0.0, alpha, nu);
+        nnn = (uint64_t)ss_lrint((double)nnn * sca) + n;
+        sca = 1.0;
+        swe = (double)nnn * unit_size;
+    }
+    if (pot_melt > unit_size) {  // 2. melting
+        uint64_t u = (uint64_t)ss_lrint(pot_melt / unit_size);
+        if (nnn < u + 2) {
+            nnn = 0;
+            alpha = alpha_0;
+            nu = alpha_0 * unit_size;
+            swe = 0.0;
+            lwc = 0.0;
+            sca = 0.0;
+        } else {
+            const double rel_red_sca = ss_sca_rel_red(u, nnn, nu, alpha, err);
+            const double sca_scale_factor = 1.0 - rel_red_sca;
+            sca = s.sca * sca_scale_factor;
+            swe = (double)(nnn - u) / sca_scale_factor * unit_size;
+            if (swe >= (double)nnn * unit_size) {
+                u = (uint64_t)((long)((double)nnn * rel_red_sca) + 1);
+                swe = (double)(nnn - u) / sca_scale_factor * unit_size;
+                if (nnn == u) sca = 0.0;
+            }
+            if (sca < 0.005) {
+                nnn = 0;
+                alpha = alpha_0;
+                nu = alpha_0 * unit_size;
+                swe = 0.0;
+                lwc = 0.0;
+                sca = 0.0;
+            } else {
+                ss_compute_shape_vars(p, nnn, n, u, sca, rel_red_sca, alpha, nu);
+                nnn = (uint64_t)ss_lrint(swe / unit_size);
+                swe = (double)nnn * unit_size;
+            }
+        }
+    }
+    // 3. lwc from the swe*sca change
+    if (s.sca * s.swe > sca * swe) lwc += smax(0.0, s.swe - swe);
+    lwc *= smin(1.0, s.sca / sca);
+    lwc = smin(lwc, swe * p.max_water_fraction);
+    double discharge = s.sca * total_storage + snow - sca * (swe + lwc);
+    if (discharge < 0.0) {
+        s.residual += discharge;
+        discharge = 0.0;
+    }
+    // 4. rain into lwc and/or discharge
+    if (rain > swe * p.max_water_fraction - lwc) {
+        discharge += sca * (rain - (swe * p.max_water_fraction - lwc)) + rain * (1.0 - sca);
+        lwc = swe * p.max_water_fraction;
+    } else {
+        lwc += rain;
+        discharge += rain * (1.0 - sca);
+    }
+    if (discharge >= -s.residual) {
+        discharge += s.residual;
+        s.residual = 0.0;
+    }
+    // 5. state and response
+    if (nnn > 0) nu /= (double)nnn;
+    r_outflow = discharge / dt_hours;
+    r_swe = sca * (swe + lwc);
+    r_sca = sca;
+    s.nu = nu;
+    s.alpha = alpha;
+    s.sca = sca;
+    s.swe = swe;
+    s.free_water = lwc;
+    s.num_units = nnn;
+}
+
+}  // namespace shyft_dev

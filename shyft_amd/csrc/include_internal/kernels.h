@@ -47,6 +47,24 @@ struct hbv_kargs {
 
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream);
 
+struct ptssk_kargs {
+    int n_cells, step0, n_steps, win0, win_len, collect;
+    double step_in_days;     // to_seconds(dt)/86400 (skaugen.h:160)
+    double dt_hours;         // to_seconds(dt)/3600 (skaugen.h:161)
+    double t1_hours;         // kirchner integration end: to_seconds(dt)/to_seconds(1h)
+    const double* params;    // [n_sets][PTSSK_NP]
+    const int32_t* set_ix;   // [N]
+    const double* cellc;     // [PTGSK_NC][N]
+    double* state;           // [PTSSK_NS][N]
+    const double* forcing;   // [N_FORCING][win_len][N]
+    double* resp;            // [n_series][win_len][N]
+    double* state_series;    // [PTSSK_NSC][win_len+1][N] or null
+    const uint8_t* active;   // [N] or null
+    int32_t* err;            // [N]
+};
+
+hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream);
+
 // synthetic workload generator, fills [5][n][N] window rows
 hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                     uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,

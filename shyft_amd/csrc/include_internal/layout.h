@@ -78,5 +78,26 @@ enum hbv_series_index {
     HR_PE_OUTPUT, HR_SOIL_OUTFLOW, HBV_NR
 };
 
+// ------------------------------------------------------------------ pt_ss_k
+// parameter row: the 21 reference values in get/set order (core/pt_ss_k.h:78-101)
+enum ptssk_param_index {
+    SK_C1 = 0, SK_C2, SK_C3, SK_AE_SCALE, SK_ALPHA0, SK_D_RANGE, SK_UNIT_SIZE, SK_MAX_WATER_FRACTION, SK_TX, SK_CX,
+    SK_TS, SK_CFR, SK_PCORR, SK_PT_ALBEDO, SK_PT_ALPHA, SK_DTF, SK_R_VELOCITY, SK_R_ALPHA, SK_R_BETA, SK_GM_DIRECT,
+    SK_RSV_DRF, PTSSK_NP
+};
+
+// pt_ss_k state (pt_ss_k.h:154-181): skaugen nu alpha sca swe free_water residual num_units, kirchner q
+enum ptssk_state_index {
+    SS_NU = 0, SS_ALPHA, SS_SCA, SS_SWE, SS_FREE_WATER, SS_RESIDUAL, SS_NUM_UNITS, SS_KIRCHNER_Q, PTSSK_NS
+};
+
+// pt_ss_k state-collector series (pt_ss_k_cell_model.h:185-200)
+enum ptssk_state_series_index {
+    SSC_KIRCHNER = 0, SSC_SCA, SSC_SWE, SSC_ALPHA, SSC_NU, SSC_LWC, SSC_RESIDUAL, PTSSK_NSC
+};
+// per-cell constants: the pt_gs_k PC_* rows (pt_ss_k.h:237-245 are the same expressions)
+// response series: the pt_gs_k PR_* ids (snow_swe = snow_total_stored_water of the all-collector)
+
 // per-cell error codes written by the stack kernels
-enum cell_error { ERR_NONE = 0, ERR_KIRCHNER_MAX_ITER = 1, ERR_NEGATIVE_OUTFLOW = 2 };
+enum cell_error { ERR_NONE = 0, ERR_KIRCHNER_MAX_ITER = 1, ERR_NEGATIVE_OUTFLOW = 2, ERR_SKAUGEN_BISECT = 3,
+                  ERR_SKAUGEN_PDF = 4 };

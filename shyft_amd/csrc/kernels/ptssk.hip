@@ -1,0 +1,156 @@
+// pt_ss_k cell kernel for gfx950.
+//
+// region_model::run_cells -> cell::run -> pt_ss_k::run (core/region_model.h:578-597,
+// core/pt_ss_k_cell_model.h:205-256, core/pt_ss_k.h:210-291) for every cell of
+// the region in ONE launch: lane = cell, the time loop inside the kernel, the
+// Skaugen snow state and kirchner q in registers, forcing read [step][cell]
+// (coalesced) and the collector series written [series][step][cell].
+//
+// Per step: p_corr -> skaugen snow -> glacier melt on the post-step sca ->
+// Priestley-Taylor -> actual evapotranspiration -> kirchner (dopri5, shared with
+// pt_gs_k) -> total discharge / charge.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../device/pt_dev.h"
+#include "../device/ptgsk_dev.h"
+#include "../device/ptssk_dev.h"
+#include "../include_internal/kernels.h"
+
+using namespace shyft_dev;
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+__global__ __launch_bounds__(BLOCK) void ptssk_run_kernel(const ptssk_kargs a) {
+    const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= a.n_cells) return;
+    if (a.active && !a.active[cell]) return;
+    const size_t N = (size_t)a.n_cells;
+    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * PTSSK_NP;
+
+    ss_par sp;
+    sp.alpha_0 = P[SK_ALPHA0];
+    sp.d_range = P[SK_D_RANGE];
+    sp.unit_size = P[SK_UNIT_SIZE];
+    sp.max_water_fraction = P[SK_MAX_WATER_FRACTION];
+    sp.tx = P[SK_TX];
+    sp.cx = P[SK_CX];
+    sp.ts = P[SK_TS];
+    sp.cfr = P[SK_CFR];
+    const double kc1 = P[SK_C1], kc2 = P[SK_C2], kc3 = P[SK_C3];
+    const double ae_scale = P[SK_AE_SCALE], p_corr = P[SK_PCORR], dtf = P[SK_DTF];
+    const double pt_albedo = P[SK_PT_ALBEDO], pt_alpha = P[SK_PT_ALPHA];
+    const double gm_direct = P[SK_GM_DIRECT];
+    const double gm_routed = 1 - gm_direct;
+
+    const double* __restrict__ cc = a.cellc;  // pt_ss_k.h:237-245 (same rows as pt_gs_k)
+    const double glacier_fraction = cc[PC_GLACIER * N + cell];
+    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + cell];
+    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + cell];
+    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + cell];
+    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + cell];
+    const double cell_area_m2 = cc[PC_AREA * N + cell];
+    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + cell];
+    const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
+
+    double* __restrict__ st = a.state;
+    ss_state s;
+    s.nu = st[SS_NU * N + cell];
+    s.alpha = st[SS_ALPHA * N + cell];
+    s.sca = st[SS_SCA * N + cell];
+    s.swe = st[SS_SWE * N + cell];
+    s.free_water = st[SS_FREE_WATER * N + cell];
+    s.residual = st[SS_RESIDUAL * N + cell];
+    s.num_units = (uint64_t)st[SS_NUM_UNITS * N + cell];
+    double q = st[SS_KIRCHNER_Q * N + cell];
+    int32_t err = 0;
+
+    const size_t TW = (size_t)a.win_len;
+    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * N;
+    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * N;
+    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * N;
+    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * N;
+    double* __restrict__ R = a.resp;
+    const size_t RS = TW * N;
+    double* __restrict__ SS = a.state_series;
+    const size_t SSS = (TW + 1) * N;
+
+    // state_collector::collect of state.scale_snow(snow_storage_fraction) (pt_ss_k_cell_model.h:185-200,
+    // pt_ss_k.h:171-177)
+    auto collect_state = [&](size_t wi) {
+        const size_t o = wi * N + cell;
+        const double swe_s = s.swe * snow_storage_fraction;
+        const double fw_s = s.free_water * snow_storage_fraction;
+        SS[SSC_KIRCHNER * SSS + o] = cell_area_m2 * q * mmh_to_m3s_scale_factor;
+        SS[SSC_SCA * SSS + o] = s.sca;
+        SS[SSC_SWE * SSS + o] = (fw_s + swe_s) * s.sca;
+        SS[SSC_ALPHA * SSS + o] = s.alpha;
+        SS[SSC_NU * SSS + o] = s.nu;
+        SS[SSC_LWC * SSS + o] = fw_s * s.sca;
+        SS[SSC_RESIDUAL * SSS + o] = s.residual;
+    };
+
+    const int i_end = a.step0 + a.n_steps;
+    for (int i = a.step0; i < i_end; ++i) {
+        const size_t wi = (size_t)(i - a.win0);
+        const size_t fo = wi * N + cell;
+        const double temp = f_temp[fo];
+        const double rad = f_rad[fo];
+        const double rel_hum = f_rh[fo];
+        const double prec = f_prec[fo] * p_corr;
+        if (SS) collect_state(wi);
+        double snow_outflow, snow_sca, snow_swe;
+        ss_step(sp, a.step_in_days, a.dt_hours, temp, prec, s, snow_outflow, snow_sca, snow_swe, err);
+        // glacier_melt::step (glacier_melt.h:47-52) on the post-step snow covered area
+        const double sca_area = cell_area_m2 * s.sca;
+        double gm_melt_m3s = 0.0;
+        if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
+            gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
+        const double pot_evap = pt_pot_evap(pt_albedo, pt_alpha, temp, rad, rel_hum) * 3600.0;
+        const double ae = pot_evap * (1.0 - dexp(-q * 3.0 / ae_scale)) * (1.0 - smax(s.sca, glacier_fraction));
+        const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
+        double q_avg;
+        if (!kirchner_step(q, q_avg, snow_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
+                           ae, a.t1_hours, kc1, kc2, kc3))
+            err = ERR_KIRCHNER_MAX_ITER;
+        const double total_discharge = smax(0.0, prec - ae) * direct_response_fraction + gm_direct * gm_mmh +
+                                       q_avg * kirchner_fraction;
+        const double charge_m3s = +(cell_area_m2 * prec * mmh_to_m3s_scale_factor) -
+                                  (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
+                                  (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        // collectors of response.scale_snow(snow_storage_fraction) (pt_ss_k.h:198-203)
+        R[PR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
+        R[PR_CHARGE_M3S * RS + fo] = charge_m3s;
+        if (a.collect >= 1) {
+            R[PR_SNOW_SCA * RS + fo] = snow_sca;
+            R[PR_SNOW_SWE * RS + fo] = snow_swe * snow_storage_fraction;
+        }
+        if (a.collect >= 2) {
+            R[PR_SNOW_OUTFLOW * RS + fo] = cell_area_m2 * (snow_outflow * snow_storage_fraction) * mmh_to_m3s_scale_factor;
+            R[PR_GLACIER_MELT * RS + fo] = gm_melt_m3s;
+            R[PR_AE_OUTPUT * RS + fo] = ae;
+            R[PR_PE_OUTPUT * RS + fo] = pot_evap;
+        }
+        if (SS && i + 1 == i_end) collect_state(wi + 1);
+    }
+    st[SS_NU * N + cell] = s.nu;
+    st[SS_ALPHA * N + cell] = s.alpha;
+    st[SS_SCA * N + cell] = s.sca;
+    st[SS_SWE * N + cell] = s.swe;
+    st[SS_FREE_WATER * N + cell] = s.free_water;
+    st[SS_RESIDUAL * N + cell] = s.residual;
+    st[SS_NUM_UNITS * N + cell] = (double)s.num_units;
+    st[SS_KIRCHNER_Q * N + cell] = q;
+    if (err) a.err[cell] = err;
+}
+
+}  // namespace
+
+hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream) {
+    const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptssk_run_kernel, dim3(grid), dim3(BLOCK), 0, stream, a);
+    return hipGetLastError();
+}

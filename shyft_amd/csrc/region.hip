@@ -133,13 +133,16 @@ struct shyft_hip_region {
     bool dst_dirty = true;
 
     bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
+    bool ptssk() const { return stack == SHYFT_HIP_PT_SS_K; }
     size_t n_series() const {
         if (collect == COLLECT_ALL) return hbv() ? HBV_NR : PTGSK_NR;
         return collect == COLLECT_DISCHARGE_SNOW ? 4 : 2;
     }
-    size_t n_state_fields() const { return hbv() ? HBV_NS : PTGSK_NS; }
-    size_t n_ref_params() const { return hbv() ? HBV_NP_REF : PTGSK_NP_REF; }
-    size_t param_width() const { return hbv() ? HBV_NP : PTGSK_NP_REF; }
+    size_t n_state_fields() const { return hbv() ? HBV_NS : (ptssk() ? PTSSK_NS : PTGSK_NS); }
+    // state-collector series per cell (pt_ss_k collects 7 series from its 8 state values)
+    size_t n_state_series() const { return ptssk() ? PTSSK_NSC : n_state_fields(); }
+    size_t n_ref_params() const { return hbv() ? HBV_NP_REF : (ptssk() ? PTSSK_NP : PTGSK_NP_REF); }
+    size_t param_width() const { return hbv() ? HBV_NP : (ptssk() ? PTSSK_NP : PTGSK_NP_REF); }
 };
 
 namespace {
@@ -221,12 +224,42 @@ void update_derived_hbv(shyft_hip_region* h) {
     h->derived_dirty = false;
 }
 
+// pt_ss_k: parameter rows as given, per-cell constants of pt_ss_k.h:237-245 in the pt_gs_k PC_* rows
+void update_derived_ptssk(shyft_hip_region* h) {
+    const size_t N = h->n;
+    std::vector<double> cc(PTGSK_NC * N, 0.0);
+    for (size_t i = 0; i < N; ++i) {
+        const double* g = &h->geo[i * 11];
+        const double* p = &h->params[size_t(h->set_ix[i]) * PTSSK_NP];
+        const double glacier = g[6], lake = g[7], reservoir = g[8];
+        const double gm_direct = p[SK_GM_DIRECT];
+        const double rdrf = p[SK_RSV_DRF];
+        const double direct = glacier * gm_direct + reservoir * rdrf;
+        cc[PC_GLACIER * N + i] = glacier;
+        cc[PC_SNOW_STORAGE * N + i] = 1.0 - lake - reservoir;
+        cc[PC_KIRCHNER_ROUTED_PREC * N + i] = reservoir * (1.0 - rdrf) + lake;
+        cc[PC_DIRECT_RESPONSE * N + i] = direct;
+        cc[PC_KIRCHNER_FRACTION * N + i] = 1 - direct;
+        cc[PC_AREA * N + i] = g[3];
+        cc[PC_GLACIER_AREA * N + i] = g[3] * glacier;
+    }
+    h->d_params.alloc(h->params.size());
+    h->d_cellc.alloc(cc.size());
+    h->d_set_ix.alloc(N);
+    hip_check(hipMemcpy(h->d_params.p, h->params.data(), h->params.size() * sizeof(double), hipMemcpyHostToDevice),
+              "upload params");
+    hip_check(hipMemcpy(h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
+    hip_check(hipMemcpy(h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
+    h->derived_dirty = false;
+}
+
 void update_derived(shyft_hip_region* h) {
     if (!h->derived_dirty) return;
     if (!h->has_geo) throw std::runtime_error("region: geo_cell_data not set");
     if (!h->has_params) throw std::runtime_error("region: parameters not set");
     if (h->dt <= 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
     if (h->hbv()) return update_derived_hbv(h);
+    if (h->ptssk()) return update_derived_ptssk(h);
     const size_t N = h->n;
     const double dt_s = double(h->dt) / 1e6;
     const double dt_in_days = dt_s / 86400.0;
@@ -282,7 +315,7 @@ void alloc_window(shyft_hip_region* h) {
     h->d_resp.alloc(h->n_series() * h->TW * N);
     hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill resp");
     if (h->collect_state) {
-        h->d_state_series.alloc(h->n_state_fields() * (h->TW + 1) * N);
+        h->d_state_series.alloc(h->n_state_series() * (h->TW + 1) * N);
         hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill state series");
     } else {
         h->d_state_series.release();
@@ -339,7 +372,7 @@ const double* series_rows(const shyft_hip_region* h, int series, size_t step0, s
         const int f = series - SHYFT_HIP_SERIES_STATE;
         if (!h->collect_state || !h->d_state_series.p)
             throw std::runtime_error(std::string(what) + ": state collection is off");
-        if (f < 0 || size_t(f) >= h->n_state_fields()) throw std::runtime_error(std::string(what) + ": invalid state field");
+        if (f < 0 || size_t(f) >= h->n_state_series()) throw std::runtime_error(std::string(what) + ": invalid state field");
         if (step0 < h->w0 || step0 + n > h->w0 + h->TW + 1)
             throw std::runtime_error(std::string(what) + ": steps outside the resident window");
         return h->d_state_series.p + (size_t(f) * (h->TW + 1) + (step0 - h->w0)) * N;
@@ -372,7 +405,7 @@ const char* shyft_hip_last_error(const shyft_hip_region* h) { return h ? h->err.
 int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_region** out) {
     if (!out) return fail(nullptr, "shyft_hip_region_create: out is null");
     *out = nullptr;
-    if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK)
+    if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK && stack != SHYFT_HIP_PT_SS_K)
         return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
     if (n_cells == 0 || n_cells > (size_t)INT32_MAX) return fail(nullptr, "shyft_hip_region_create: invalid n_cells");
     std::unique_ptr<shyft_hip_region> h(new shyft_hip_region());
@@ -450,6 +483,8 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
         if (h->hbv()) {
             if (n_per_set != HBV_NP_REF && n_per_set != HBV_NP)
                 throw std::runtime_error("HBV_Stack Parameter Accessor: .set size missmatch");
+        } else if (h->ptssk()) {
+            if (n_per_set != PTSSK_NP) throw std::runtime_error("pt_ss_k parameter accessor: .set size mismatch");
         } else if (n_per_set != h->n_ref_params()) {
             throw std::runtime_error("PTGSK Parameter Accessor: .set size missmatch");
         }
@@ -545,7 +580,7 @@ int shyft_hip_set_collection(shyft_hip_region* h, int collect, int collect_state
             h->d_resp.alloc(h->n_series() * h->TW * N);
             hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill resp");
             if (h->collect_state) {
-                h->d_state_series.alloc(h->n_state_fields() * (h->TW + 1) * N);
+                h->d_state_series.alloc(h->n_state_series() * (h->TW + 1) * N);
                 hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill");
             } else {
                 h->d_state_series.release();
@@ -741,6 +776,32 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     size_t b = n_steps > 0 ? size_t(start_step) : 0;
     size_t e = n_steps > 0 ? size_t(start_step + n_steps) : h->T;
     check_window(h, b, e - b, "run_cells");
+    if (h->ptssk()) {
+        ptssk_kargs a;
+        a.n_cells = int(h->n);
+        a.step0 = int(b);
+        a.n_steps = int(e - b);
+        a.win0 = int(h->w0);
+        a.win_len = int(h->TW);
+        a.collect = h->collect;
+        const double dt_s = double(h->dt) / 1e6;  // to_seconds(period.timespan())
+        a.step_in_days = dt_s / 86400.0;
+        a.dt_hours = dt_s / 3600.0;
+        a.t1_hours = dt_s / 3600.0;
+        a.params = h->d_params.p;
+        a.set_ix = h->d_set_ix.p;
+        a.cellc = h->d_cellc.p;
+        a.state = h->d_state.p;
+        a.forcing = h->d_forcing.p;
+        a.resp = h->d_resp.p;
+        a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
+        a.active = h->active.empty() ? nullptr : h->d_active.p;
+        a.err = h->d_err.p;
+        hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
+        hip_check(launch_ptssk_run(a, h->stream), "ptssk_run_kernel launch");
+        hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
+        return;
+    }
     if (h->hbv()) {
         hbv_kargs a;
         a.n_cells = int(h->n);
@@ -806,6 +867,13 @@ static void finish_run(shyft_hip_region* h) {
             if (errs[i] == ERR_NEGATIVE_OUTFLOW)
                 throw std::runtime_error("Negative outflow: total_water - swe < -1e-6 in hbv_snow (cell " +
                                          std::to_string(i) + ")");
+            if (errs[i] == ERR_SKAUGEN_BISECT)
+                throw std::runtime_error("No change of sign in boost::math::tools::bisect, either there is no root to "
+                                         "find, or there are multiple roots in the interval (skaugen sca_rel_red, cell " +
+                                         std::to_string(i) + ")");
+            if (errs[i] == ERR_SKAUGEN_PDF)
+                throw std::runtime_error("boost::math::pdf(gamma_distribution): overflow at x = 0 (skaugen sca_rel_red, "
+                                         "cell " + std::to_string(i) + ")");
             throw std::runtime_error("kirchner: Max number of iterations exceeded (500). A new step size was not found. (cell " +
                                      std::to_string(i) + ")");
         }
@@ -861,7 +929,7 @@ int shyft_hip_get_state_series(const shyft_hip_region* hc, int field, size_t ste
     if (!h || !dst) return fail(h, "shyft_hip_get_state_series: null argument");
     return guarded(h, [&] {
         if (!h->collect_state) throw std::runtime_error("get_state_series: state collection is off");
-        if (field < 0 || size_t(field) >= h->n_state_fields()) throw std::runtime_error("get_state_series: invalid field");
+        if (field < 0 || size_t(field) >= h->n_state_series()) throw std::runtime_error("get_state_series: invalid field");
         if (step0 < h->w0 || step0 + n > h->w0 + h->TW + 1) throw std::runtime_error("get_state_series: outside window");
         const double* src = h->d_state_series.p + (size_t(field) * (h->TW + 1) + (step0 - h->w0)) * h->n;
         copy_rows(h->stream, dst, src, n * h->n * sizeof(double), dst_on_device, 1);

@@ -26,9 +26,13 @@ HBV_MAX_BINS = 8
 HBV_STATE = (("swe", "sca", "soil_moisture", "tank_uz", "tank_lz", "n_bins") +
              tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) + tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
 SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
-STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22}
-STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE)}
-STACK_NSERIES = {PT_GS_K: len(PTGSK_SERIES), HBV_STACK: len(HBV_SERIES)}
+# pt_ss_k (core/pt_ss_k.h:154-181, pt_ss_k_cell_model.h:38-200); response series ids are the pt_gs_k ones
+PTSSK_STATE = ("nu", "alpha", "sca", "swe", "free_water", "residual", "num_units", "kirchner_q")
+PTSSK_STATE_SERIES = ("kirchner_discharge", "snow_sca", "snow_swe", "snow_alpha", "snow_nu", "snow_lwc",
+                      "snow_residual")
+STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22, PT_SS_K: 21}
+STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE), PT_SS_K: len(PTSSK_STATE)}
+STACK_NSERIES = {PT_GS_K: len(PTGSK_SERIES), HBV_STACK: len(HBV_SERIES), PT_SS_K: len(PTGSK_SERIES)}
 
 
 def _ptr(a: np.ndarray | None):

@@ -140,3 +140,30 @@ def default_hbv_state(n_cells: int, uz: float = 40.0, lz: float = 40.0) -> np.nd
     s[:, 3] = uz
     s[:, 4] = lz
     return s
+
+
+def default_ptssk_parameters() -> np.ndarray:
+    """PTSSKParameter() defaults in the reference get/set order (core/pt_ss_k.h:78-101)."""
+    return np.array([
+        -2.439, 0.966, -0.10,                                # kirchner c1 c2 c3
+        1.5,                                                 # ae.ae_scale_factor
+        40.77, 113.0, 0.1, 0.1, 0.16, 2.5, 0.14, 0.01,       # ss alpha_0 d_range unit_size max_water_fraction tx cx ts cfr
+        1.0,                                                 # p_corr.scale_factor
+        0.2, 1.26,                                           # pt.albedo pt.alpha
+        6.0,                                                 # gm.dtf
+        1.0, 7.0, 0.0,                                       # routing velocity alpha beta
+        0.0,                                                 # gm.direct_response
+        1.0,                                                 # msp.reservoir_direct_response_fraction
+    ], dtype=np.float64)
+
+
+PTSSK_NS = 8  # nu alpha sca swe free_water residual num_units kirchner.q
+
+
+def default_ptssk_state(n_cells: int, q: float = 1.0) -> np.ndarray:
+    """PTSSKState(): skaugen::state() (skaugen.h:122-124: nu 4.077, alpha 40.77, no snow) with kirchner.q = q."""
+    s = np.zeros((n_cells, PTSSK_NS), dtype=np.float64)
+    s[:, 0] = 4.077
+    s[:, 1] = 40.77
+    s[:, 7] = q
+    return s

@@ -88,3 +88,37 @@ def run_hbv(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n
         return out
     finally:
         r.close()
+
+
+def run_ptssk(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, full=True,
+              collect_state=False):
+    """pt_ss_k region; forcing [5][T][N]; params [n_sets][21]; state [N][8].
+    Returns dict main [2][T][N], full [8][T][N], state [N][8] (+ state_series [7][T+1][N])."""
+    geo11 = np.atleast_2d(geo11)
+    if engine == "oracle":
+        return oracle_lib.ptssk_run(geo11, params, state, t0_us, dt_us, forcing, start_step, n_steps, set_ix, full=full,
+                                    collect_state=collect_state)
+    from shyft_amd.region import HipRegion, PT_SS_K, COLLECT_ALL, COLLECT_DISCHARGE, PTSSK_STATE, PTSSK_STATE_SERIES
+    N = geo11.shape[0]
+    T = forcing.shape[1]
+    r = HipRegion(PT_SS_K, N)
+    try:
+        r.set_geo(geo11)
+        r.set_parameters(np.atleast_2d(params), set_ix)
+        r.set_time_axis(t0_us, dt_us, T)
+        r.set_collection(COLLECT_ALL if full else COLLECT_DISCHARGE, collect_state)
+        r.set_state(np.asarray(state).reshape(N, len(PTSSK_STATE)))
+        for v in range(5):
+            r.set_forcing(v, 0, forcing[v])
+        r.run_cells(0, start_step, n_steps)
+        out = {"state": r.get_state()}
+        ns = 8 if full else 2
+        allser = np.stack([r.get_series(k, 0, T) for k in range(ns)])
+        out["main"] = allser[:2]
+        if full:
+            out["full"] = allser
+        if collect_state:
+            out["state_series"] = np.stack([r.get_state_series(k, 0, T + 1) for k in range(len(PTSSK_STATE_SERIES))])
+        return out
+    finally:
+        r.close()

@@ -76,8 +76,61 @@ def load(variant: str = "detmath"):
     L.oracle_hbv_run.argtypes = ([C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                   C.c_int64, C.c_int64, C.c_size_t, C.c_int, C.c_int] + [C.c_void_p] * 8 +
                                  [C.c_int, _dp, C.c_char_p, C.c_size_t])
+    L.oracle_skaugen_step.restype = C.c_int
+    L.oracle_skaugen_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, _d, _d]
+    L.oracle_skaugen_sca_rel_red.restype = _d
+    L.oracle_skaugen_sca_rel_red.argtypes = [C.c_uint64, C.c_uint64, _d, _d]
+    L.oracle_ptssk_run.restype = C.c_int
+    L.oracle_ptssk_run.argtypes = L.oracle_ptgsk_run.argtypes
     _CACHE[variant] = L
     return L
+
+
+SKAUGEN_DEFAULT = (40.77, 113.0, 0.1, 0.1, 0.16, 2.5, 0.14, 0.01)  # skaugen::parameter() (skaugen.h:89-112)
+PTSSK_NS = 8        # nu alpha sca swe free_water residual num_units kirchner.q
+PTSSK_NSC = 7       # state collector series (pt_ss_k_cell_model.h:185-200)
+
+
+def skaugen_step(state7, dt_us, T, prec_mm_h, p8=SKAUGEN_DEFAULT, variant="detmath"):
+    """One skaugen::calculator::step; state7 (nu alpha sca swe free_water residual num_units) updated in place.
+    Returns (outflow, sca, swe) of the response."""
+    L = load(variant)
+    st = np.ascontiguousarray(state7, dtype=np.float64)
+    p = np.ascontiguousarray(p8, dtype=np.float64)
+    r = np.zeros(3)
+    if L.oracle_skaugen_step(_p(st), _p(r), int(dt_us), _p(p), float(T), float(prec_mm_h)) != 0:
+        raise RuntimeError("skaugen step raised")
+    state7[:] = st
+    return tuple(r)
+
+
+def ptssk_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, full=False,
+              collect_state=False, ncore=0, variant="detmath"):
+    """pt_ss_k region on the oracle: 'main' [2][T][N], 'full' [8][T][N], 'state_series' [7][T+1][N], 'state' [N][8]."""
+    L = load(variant)
+    geo11 = np.ascontiguousarray(geo11, dtype=np.float64)
+    N = geo11.shape[0]
+    params = np.ascontiguousarray(np.atleast_2d(params), dtype=np.float64)
+    st = np.ascontiguousarray(state, dtype=np.float64).reshape(N, PTSSK_NS).copy()
+    F = np.ascontiguousarray(forcing, dtype=np.float64)
+    T = F.shape[1]
+    ix = None if set_ix is None else np.ascontiguousarray(set_ix, dtype=np.int32)
+    out_main = np.empty((2, T, N))
+    out_full = np.empty((8, T, N)) if full else None
+    out_state = np.empty((PTSSK_NSC, T + 1, N)) if collect_state else None
+    el = C.c_double(0.0)
+    err = C.create_string_buffer(512)
+    rc = L.oracle_ptssk_run(N, _p(geo11), _p(params), params.shape[0], _p(ix), _p(st), int(t0_us), int(dt_us), T,
+                            int(start_step), int(n_steps), _p(F[0]), _p(F[1]), _p(F[2]), _p(F[3]), _p(F[4]),
+                            _p(out_main), _p(out_full), _p(out_state), int(ncore), C.byref(el), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    r = {"main": out_main, "state": st, "elapsed_s": el.value}
+    if full:
+        r["full"] = out_full
+    if collect_state:
+        r["state_series"] = out_state
+    return r
 
 
 def _p(a):
