@@ -284,6 +284,7 @@ PYBIND11_MODULE(_api, m) {
 
     bind_model<pt_gs_k_stack>(m, "_PTGSKRegionModel");
     bind_model<hbv_stack_stack>(m, "_HbvRegionModel");
+    bind_model<pt_ss_k_stack>(m, "_PTSSKRegionModel");
 
     py::register_exception_translator([](std::exception_ptr p) {
         try {

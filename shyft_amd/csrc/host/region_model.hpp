@@ -161,6 +161,18 @@ struct hbv_stack_stack {
     static constexpr const char* param_error = "HBV_Stack Parameter Accessor: .set size missmatch";
 };
 
+struct pt_ss_k_stack {
+    static constexpr int id = SHYFT_HIP_PT_SS_K;
+    static constexpr size_t n_param = 21;   // core/pt_ss_k.h:74
+    static constexpr size_t n_state = 8;    // skaugen nu alpha sca swe free_water residual num_units + kirchner.q
+    static constexpr size_t n_full_series = 8;
+    static constexpr int k_ae_scale = 3;
+    static constexpr int k_routing = 16;
+    static constexpr int state_q = 7;
+    static constexpr double q_min = 0.0;
+    static constexpr const char* param_error = "pt_ss_k parameter accessor: .set size mismatch";
+};
+
 // ---- region_model ------------------------------------------------------------------------------------------------
 template <class Stack>
 class region_model {
@@ -220,6 +232,8 @@ class region_model {
     static state_t default_state() {
         if (Stack::id == SHYFT_HIP_PT_GS_K)  // gamma_snow::state() + kirchner::state() (gamma_snow.h:101-116, kirchner.h:131)
             return {0.4, 0.1, 30000.0, 1.26, 0.0, 0.0, 0.0, 0.0, 0.1};
+        if (Stack::id == SHYFT_HIP_PT_SS_K)  // skaugen::state() (skaugen.h:122-124) + kirchner::state()
+            return {4.077, 40.77, 0.0, 0.0, 0.0, 0.0, 0.0, 0.1};
         state_t s(Stack::n_state, 0.0);  // hbv_stack::state(): snow undistributed, soil sm 0, tank uz 20 lz 10
         s[3] = 20.0;                    // (hbv_soil.h:28, hbv_tank.h:32)
         s[4] = 10.0;

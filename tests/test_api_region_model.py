@@ -227,3 +227,50 @@ def test_hbv_model_discharge():
     assert model.statistics.discharge_value(cids, 0) >= 32.0
     assert model.hbv_snow_state.swe(cids).size() == ta.size() + 1
     assert math.isfinite(model.hbv_tank_state.uz_value(cids, 10))
+
+
+def test_pt_ss_k_model_init_and_run():
+    """test_region_model_stacks.py:71-78 (pt_ss_k model init) plus a run through the same dummy environment:
+    the API model's discharge equals the C-ABI region run on the interpolated forcing (oracle-checked kernel)."""
+    from shyft_amd import api
+    from shyft_amd.api import pt_ss_k
+    n = 20
+    model = build_model(pt_ss_k.PTSSKModel, pt_ss_k.PTSSKParameter, n)
+    assert model.size() == n
+    assert model.skaugen_snow_response is not None and model.skaugen_snow_state is not None
+    cal = api.Calendar()
+    ta = api.TimeAxisFixedDeltaT(cal.time(2015, 1, 1, 0, 0, 0), api.deltahours(1), 240)
+    model.initialize_cell_environment(ta)
+    model.interpolate(interpolation_parameter(), dummy_env(ta, model.get_cells()[n // 2].geo.mid_point()))
+    s0 = pt_ss_k.PTSSKStateVector()
+    for _ in range(n):
+        si = pt_ss_k.PTSSKState()
+        si.kirchner.q = 40.0
+        s0.append(si)
+    model.set_states(s0)
+    model.set_state_collection(-1, True)
+    model.run_cells()
+    cids = api.IntVector()
+    q = model.statistics.discharge(cids).values.to_numpy()
+    assert np.all(np.isfinite(q)) and q[0] > 0
+    # 10 degC rain-on-bare-ground: no snow state appears
+    assert model.skaugen_snow_state.swe(cids).values.to_numpy().max() == 0.0
+    assert model.skaugen_snow_response.outflow_value(cids, 5) >= 0.0
+    # the same region through the C ABI directly
+    from shyft_amd.region import HipRegion, PT_SS_K, COLLECT_DISCHARGE
+    r = HipRegion(PT_SS_K, n)
+    geo = np.zeros((n, 11))
+    for i in range(n):
+        geo[i] = [500 + 1000.0 * i, 500.0, 500.0 * i / n, 1e6, 1, 0.9, 0.01, 0.05, 0.19, 0.30, 0.45]
+    r.set_geo(geo)
+    r.set_parameters(np.array(pt_ss_k.PTSSKParameter().to_vector()))
+    r.set_time_axis(ta.start * 10**6, 3600 * 10**6, 240)
+    r.set_collection(COLLECT_DISCHARGE)
+    st = np.tile(np.array(pt_ss_k.PTSSKState().to_vector()), (n, 1))
+    st[:, 7] = 40.0
+    r.set_state(st)
+    for v in range(5):
+        r.set_forcing(v, 0, np.stack([model.cells[i].env_ts.__getattr__(api.FORCING[v]).to_numpy()
+                                      for i in range(n)], axis=1))
+    r.run_cells()
+    assert np.allclose(r.get_series(0, 0, 240).sum(axis=1), q, rtol=1e-13, atol=0)
