@@ -171,6 +171,25 @@ int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t s
  * calculated cell (catchment filter) in the resident window is NaN. */
 int shyft_hip_forcing_ok(const shyft_hip_region* h, int* ok);
 
+/* ---- routing::uhg river aggregation (core/routing.h:239-421; region_model.h:909-949) ----
+ * Convolution is linear, so the engine reduces the avg_discharge of all cells that share a river
+ * and a unit hydrograph ("routing group") to one sum per group on the device, and convolves only
+ * those sums. */
+
+/* group_of_cell[n_cells]: the routing group of each cell, -1 = not routed (routing.id <= 0). */
+int shyft_hip_set_routing_groups(shyft_hip_region* h, const int32_t* group_of_cell, size_t n_groups);
+/* dst[n_groups][n]: sum over each group's cells (cell order) of avg_discharge, steps [step0, step0+n). */
+int shyft_hip_routing_group_sums(const shyft_hip_region* h, size_t step0, size_t n, double* dst, int dst_on_device);
+/* River network evaluation on a device (stateless; device < 0 = current): rivers are indexed 0..R-1 in
+ * ascending river id. group_sums[G][T] (host or device), group_uhg[G][max_len] / group_len[G] the cell UHG
+ * of each group (make_uhg_from_gamma, routing.h:399-421), group_river[G] its river, river_uhg[R][max_len] /
+ * river_len[R], river_downstream[R] (index, -1 = none). Outputs [R][T]: local_inflow, upstream_inflow,
+ * output_m3s (routing::model::local_inflow / upstream_inflow / output_m3s, routing.h:347-387). */
+int shyft_hip_route(int device, size_t n_groups, size_t T, const double* group_sums, int src_on_device,
+                    const double* group_uhg, const int32_t* group_len, const int32_t* group_river, size_t n_rivers,
+                    const double* river_uhg, const int32_t* river_len, const int32_t* river_downstream, size_t max_len,
+                    double* local, double* upstream, double* output, int dst_on_device);
+
 /* Diagnostic: evaluate one device elementary function (0 exp, 1 log, 2 pow(x, y), 3 lgamma,
  * 4 gamma_p(x, y)) on n host inputs on the current device; out[n] host. Used by the parity
  * tests to show device math == host math bit for bit. */

@@ -406,3 +406,39 @@ int oracle_hbv_run(size_t n_cells, const double* geo11, const double* params, co
 }
 
 }  // extern "C"
+
+// routing::model query (core/routing.h:347-387) for river `query`: local, upstream, output [T].
+//  q [T][N] avg_discharge; per cell: routing id, distance, (velocity, alpha, beta) of its parameter;
+//  per river: id, downstream id, downstream distance, (velocity, alpha, beta).
+#include "routing.hpp"
+extern "C" int oracle_route(size_t n_cells, size_t T, int64_t dt_us, const double* q, const int64_t* cell_rid,
+                            const double* cell_dist, const double* cell_vab, size_t n_rivers, const int64_t* rid,
+                            const int64_t* ds, const double* rdist, const double* rvab, int64_t query, double* local,
+                            double* upstream, double* output) {
+    try {
+        routing::model m;
+        m.T = T;
+        m.dt_us = dt_us;
+        for (size_t r = 0; r < n_rivers; ++r)
+            m.rivers[rid[r]] = routing::river{rid[r], ds[r], rdist[r], rvab[3 * r], rvab[3 * r + 1], rvab[3 * r + 2]};
+        for (size_t i = 0; i < n_cells; ++i)
+            if (cell_rid[i] > 0)
+                m.cells.push_back(routing::cell_route{cell_rid[i], cell_dist[i], cell_vab[3 * i], cell_vab[3 * i + 1],
+                                                      cell_vab[3 * i + 2], q + i, n_cells});
+        auto a = m.local_inflow(query);
+        auto b = m.upstream_inflow(query);
+        auto c = m.output(query);
+        std::copy(a.begin(), a.end(), local);
+        std::copy(b.begin(), b.end(), upstream);
+        std::copy(c.begin(), c.end(), output);
+    } catch (...) {
+        return 1;
+    }
+    return 0;
+}
+
+extern "C" void oracle_make_uhg(int n_steps, double alpha, double beta, double* out, int* len) {
+    auto w = routing::make_uhg_from_gamma(n_steps, alpha, beta);
+    std::copy(w.begin(), w.end(), out);
+    *len = int(w.size());
+}

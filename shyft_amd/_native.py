@@ -53,6 +53,11 @@ SIGNATURES = {
     "shyft_hip_region_clone": (C.c_int, [_h, C.POINTER(C.c_void_p)]),
     "shyft_hip_cell_series": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
     "shyft_hip_forcing_ok": (C.c_int, [_h, C.POINTER(C.c_int)]),
+    "shyft_hip_set_routing_groups": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
+    "shyft_hip_routing_group_sums": (C.c_int, [_h, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
+    "shyft_hip_route": (C.c_int, [C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_int]),
     "shyft_hip_math_selftest": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
 }
 

@@ -607,9 +607,9 @@ class region_model {
         return false;
     }
     // the three river flows; on a model without routing they are 0-series on the time axis
-    std::vector<double> river_output_flow_m3s(int64_t rid) const { return routed(rid).output(rid); }
-    std::vector<double> river_upstream_inflow_m3s(int64_t rid) const { return routed(rid).upstream_inflow(rid); }
-    std::vector<double> river_local_inflow_m3s(int64_t rid) const { return routed(rid).local_inflow(rid); }
+    std::vector<double> river_output_flow_m3s(int64_t rid) const { return routed(rid, 2); }
+    std::vector<double> river_upstream_inflow_m3s(int64_t rid) const { return routed(rid, 1); }
+    std::vector<double> river_local_inflow_m3s(int64_t rid) const { return routed(rid, 0); }
 
   private:
     std::shared_ptr<shyft_hip_region> h_;
@@ -712,36 +712,70 @@ class region_model {
         throw_if(shyft_hip_interpolate(h_.get(), var, S, xyz.data(), vals.data(), 0, T, prm), h_.get());
     }
 
-    routing_model routed(int64_t rid) const {
-        if (!has_routing()) return routing_model::zero(time_axis, rivers);
+    // routing::model over the device (routing.h:239-387): which = 0 local_inflow, 1 upstream_inflow, 2 output_m3s
+    std::vector<double> routed(int64_t rid, int which) const {
+        const size_t T = time_axis.size();
+        if (!has_routing()) return std::vector<double>(T, 0.0);
         rivers.check_rid(rid);
-        // the routing model aggregates on device: per (river, uhg) group sums of avg_discharge
+        // routing groups: cells sharing (river, UHG length, alpha, beta) (routing.h:326-330)
         std::vector<uhg_group> groups;
-        std::vector<int64_t> group_of(size(), -1);
+        std::vector<int32_t> group_of(size(), -1);
         std::map<std::tuple<int64_t, int, double, double>, size_t> key_to_group;
         for (size_t i = 0; i < size(); ++i) {
             const auto& g = geo_[i];
             if (!valid_routing_id(g.routing.id)) continue;
             if (!catchment_filter_.empty() && !catchment_filter_[cid_to_cix_.at(g.catchment_id())]) continue;
+            rivers.check_rid(g.routing.id);  // routing::model::verify_cell_river_connections (routing.h:313-320)
             const auto& p = cell_parameter(i);
             const double velocity = p[Stack::k_routing], alpha = p[Stack::k_routing + 1], beta = p[Stack::k_routing + 2];
-            const int n_steps = uhg_steps(g.routing.distance, velocity, time_axis.dt);  // routing.h:326-330
+            const int n_steps = uhg_steps(g.routing.distance, velocity, time_axis.dt);
             auto key = std::make_tuple(g.routing.id, n_steps, alpha, beta);
             auto f = key_to_group.find(key);
             if (f == key_to_group.end()) {
                 f = key_to_group.emplace(key, groups.size()).first;
                 groups.push_back(uhg_group{g.routing.id, make_uhg_from_gamma(n_steps, alpha, beta), {}});
             }
-            group_of[i] = int64_t(f->second);
+            group_of[i] = int32_t(f->second);
         }
-        // group discharge sums on device: per-group select_sum of avg_discharge, group cells in cell order
-        for (size_t k = 0; k < groups.size(); ++k) {
-            std::vector<int64_t> cells;
-            for (size_t i = 0; i < size(); ++i)
-                if (group_of[i] == int64_t(k)) cells.push_back(int64_t(i));
-            groups[k].q = stat_series(SHYFT_HIP_AVG_DISCHARGE, cells, SHYFT_HIP_SCOPE_CELL_IX, false);
+        const size_t G = groups.size();
+        std::vector<double> sums(G * T);
+        throw_if(shyft_hip_set_routing_groups(h_.get(), group_of.data(), G), h_.get());
+        if (G) throw_if(shyft_hip_routing_group_sums(h_.get(), 0, T, sums.data(), 0), h_.get());
+        // rivers indexed in ascending id (the rid_map order)
+        std::vector<int64_t> ids;
+        std::map<int64_t, int32_t> index_of;
+        for (const auto& kv : rivers.rid_map) {
+            index_of[kv.first] = int32_t(ids.size());
+            ids.push_back(kv.first);
         }
-        return routing_model(time_axis, rivers, std::move(groups));
+        const size_t R = ids.size();
+        std::vector<std::vector<double>> rw(R);
+        size_t max_len = 1;
+        for (size_t r = 0; r < R; ++r) {
+            rw[r] = rivers.rid_map.at(ids[r]).uhg(time_axis.dt);
+            max_len = std::max(max_len, rw[r].size());
+        }
+        for (const auto& g : groups) max_len = std::max(max_len, g.w.size());
+        std::vector<double> gw(G * max_len, 0.0), rwf(R * max_len, 0.0);
+        std::vector<int32_t> glen(G), griver(G), rlen(R), rdown(R);
+        for (size_t k = 0; k < G; ++k) {
+            std::copy(groups[k].w.begin(), groups[k].w.end(), gw.begin() + k * max_len);
+            glen[k] = int32_t(groups[k].w.size());
+            griver[k] = index_of.at(groups[k].rid);
+        }
+        for (size_t r = 0; r < R; ++r) {
+            std::copy(rw[r].begin(), rw[r].end(), rwf.begin() + r * max_len);
+            rlen[r] = int32_t(rw[r].size());
+            const int64_t ds = rivers.rid_map.at(ids[r]).downstream_id;
+            rdown[r] = valid_routing_id(ds) ? index_of.at(ds) : -1;
+        }
+        std::vector<double> local(R * T), up(R * T), out(R * T);
+        throw_if(shyft_hip_route(-1, G, T, sums.data(), 0, gw.data(), glen.data(), griver.data(), R, rwf.data(),
+                                 rlen.data(), rdown.data(), max_len, local.data(), up.data(), out.data(), 0),
+                 nullptr);
+        const auto& sel = which == 0 ? local : (which == 1 ? up : out);
+        const size_t r = size_t(index_of.at(rid));
+        return std::vector<double>(sel.begin() + r * T, sel.begin() + (r + 1) * T);
     }
 
     void clone_from(const region_model& o, bool full_collection) {

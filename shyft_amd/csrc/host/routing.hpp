@@ -10,10 +10,11 @@
 // MI355X design: convolution is linear, so the per-cell convolutions of all cells
 // sharing (river, UHG) collapse to ONE convolution of their summed discharge.
 // The engine reduces avg_discharge over each (river, UHG) group on the device
-// (shyft_hip_statistics, HBM-bound, 8 B per cell-step); only the [groups][T]
-// sums reach the host, where the per-group and per-river convolutions and the
-// (small) network recursion run. Results equal the reference up to the order of
-// floating-point additions.
+// (shyft_hip_routing_group_sums, HBM-bound, 8 B per cell-step) and evaluates the
+// group and river convolutions level by level through the network on the device
+// (shyft_hip_route, kernels/routing.hip). This header holds the host-side pieces:
+// the river network bookkeeping and the UHG weights. Results equal the reference
+// up to the order of floating-point additions.
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -86,17 +87,6 @@ inline std::vector<double> make_uhg_from_gamma(int n_steps, double alpha, double
 inline int uhg_steps(double distance, double velocity, utctimespan dt) {
     const double steps = (distance / velocity) / to_seconds(dt);
     return int(steps + 0.5);
-}
-
-// convolve_w_ts with convolve_policy::USE_ZERO (time_series.h:966-974)
-inline std::vector<double> convolve_use_zero(const std::vector<double>& ts, const std::vector<double>& w) {
-    std::vector<double> r(ts.size(), 0.0);
-    for (size_t i = 0; i < ts.size(); ++i) {
-        double v = 0.0;
-        for (size_t j = 0; j < w.size(); ++j) v += j <= i ? w[j] * ts[i - j] : 0.0;
-        r[i] = v;
-    }
-    return r;
 }
 
 struct river {  // routing.h:94-124
@@ -200,46 +190,6 @@ struct uhg_group {
     int64_t rid = 0;
     std::vector<double> w;
     std::vector<double> q;
-};
-
-// routing::model (routing.h:239-387) over the device-reduced group sums
-class routing_model {
-  public:
-    routing_model(const fixed_dt& ta, const river_network& rn, std::vector<uhg_group> groups)
-        : ta_(ta), rn_(rn), groups_(std::move(groups)) {}
-    static routing_model zero(const fixed_dt& ta, const river_network& rn) { return routing_model(ta, rn, {}); }
-
-    std::vector<double> local_inflow(int64_t rid) const {
-        std::vector<double> r(ta_.size(), 0.0);
-        for (const auto& g : groups_)
-            if (g.rid == rid) {
-                auto o = convolve_use_zero(g.q, g.w);
-                for (size_t t = 0; t < r.size(); ++t) r[t] += o[t];
-            }
-        return r;
-    }
-    std::vector<double> upstream_inflow(int64_t rid) const {
-        std::vector<double> r(ta_.size(), 0.0);
-        if (groups_.empty()) return r;
-        for (auto up : rn_.upstreams_by_id(rid)) {
-            auto o = output(up);
-            for (size_t t = 0; t < r.size(); ++t) r[t] += o[t];
-        }
-        return r;
-    }
-    std::vector<double> output(int64_t rid) const {
-        if (groups_.empty()) return std::vector<double>(ta_.size(), 0.0);
-        auto w = rn_.river_by_id(rid).uhg(ta_.dt);
-        auto a = local_inflow(rid);
-        auto b = upstream_inflow(rid);
-        for (size_t t = 0; t < a.size(); ++t) a[t] += b[t];
-        return convolve_use_zero(a, w);
-    }
-
-  private:
-    fixed_dt ta_;
-    const river_network& rn_;
-    std::vector<uhg_group> groups_;
 };
 
 }  // namespace shyft_hip::host

@@ -65,6 +65,26 @@ struct ptssk_kargs {
 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream);
 
+// routing (kernels/routing.hip): river aggregation of (river, UHG) group discharge sums
+struct routing_args {
+    int n_steps, n_rivers, max_len;
+    const double* group_sums;       // [G][n_steps]
+    const double* group_w;          // [G][max_len] UHG taps (zero padded)
+    const int32_t* group_len;       // [G]
+    const int32_t* river_group_off; // [R+1] CSR of the groups of each river (ascending group index)
+    const int32_t* river_groups;
+    const double* river_w;          // [R][max_len]
+    const int32_t* river_len;       // [R]
+    const int32_t* river_up_off;    // [R+1] CSR of upstream rivers (ascending river id)
+    const int32_t* river_up;
+    const int32_t* level_rivers;    // rivers ordered by network level (upstream levels first)
+    double* local;                  // [R][n_steps] local_inflow
+    double* upstream;               // [R][n_steps] upstream_inflow
+    double* inflow;                 // [R][n_steps] local + upstream (scratch)
+    double* output;                 // [R][n_steps] output_m3s
+};
+hipError_t launch_route(const routing_args& a, const int* level_off, int n_levels, hipStream_t stream);
+
 // synthetic workload generator, fills [5][n][N] window rows
 hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                     uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,

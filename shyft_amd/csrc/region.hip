@@ -132,6 +132,10 @@ struct shyft_hip_region {
     dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
     bool dst_dirty = true;
 
+    // routing groups (cells sharing river + UHG): segment tables for the group discharge sums
+    dbuf<int32_t> d_rseg_cells, d_rseg_off;
+    size_t n_route_groups = 0;
+
     bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
     bool ptssk() const { return stack == SHYFT_HIP_PT_SS_K; }
     size_t n_series() const {
@@ -1066,6 +1070,169 @@ int shyft_hip_forcing_ok(const shyft_hip_region* hc, int* ok) {
         hip_check(hipStreamSynchronize(h->stream), "sync");
         *ok = flag ? 0 : 1;
     });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- routing (core/routing.h:239-421)
+extern "C" {
+
+int shyft_hip_set_routing_groups(shyft_hip_region* h, const int32_t* group_of_cell, size_t n_groups) {
+    if (!h) return fail(h, "shyft_hip_set_routing_groups: null handle");
+    return guarded(h, [&] {
+        if (n_groups > 0 && !group_of_cell) throw std::runtime_error("set_routing_groups: group_of_cell is null");
+        std::vector<int32_t> off(n_groups + 1, 0), cells;
+        for (size_t i = 0; i < h->n && n_groups; ++i) {
+            const int32_t g = group_of_cell[i];
+            if (g < -1 || g >= int32_t(n_groups)) throw std::runtime_error("set_routing_groups: group index out of range");
+            if (g >= 0) off[size_t(g) + 1]++;
+        }
+        for (size_t g = 0; g < n_groups; ++g) off[g + 1] += off[g];
+        cells.resize(size_t(off[n_groups]));
+        std::vector<int32_t> pos(off.begin(), off.end() - 1);
+        for (size_t i = 0; i < h->n && n_groups; ++i)
+            if (group_of_cell[i] >= 0) cells[size_t(pos[size_t(group_of_cell[i])]++)] = int32_t(i);
+        h->d_rseg_off.alloc(n_groups + 1);
+        h->d_rseg_cells.alloc(std::max<size_t>(1, cells.size()));
+        hip_check(hipMemcpy(h->d_rseg_off.p, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
+        if (!cells.empty())
+            hip_check(hipMemcpy(h->d_rseg_cells.p, cells.data(), cells.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+                      "upload");
+        h->n_route_groups = n_groups;
+    });
+}
+
+int shyft_hip_routing_group_sums(const shyft_hip_region* hc, size_t step0, size_t n, double* dst, int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_routing_group_sums: null argument");
+    return guarded(h, [&] {
+        const size_t G = h->n_route_groups;
+        if (G == 0) return;
+        const double* src = series_rows(h, SHYFT_HIP_AVG_DISCHARGE, step0, n, "routing_group_sums");
+        double* out = dst;
+        if (!dst_on_device) {
+            h->d_tmp.alloc(std::max(h->d_tmp.n, G * n));
+            out = h->d_tmp.p;
+        }
+        hip_check(launch_segment_sums(src, h->n, n, h->d_rseg_cells.p, h->d_rseg_off.p, G, out, h->stream),
+                  "routing group sums");
+        if (!dst_on_device) copy_rows(h->stream, dst, out, G * n * sizeof(double), 0, 1);
+        else hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_route(int device, size_t n_groups, size_t T, const double* group_sums, int src_on_device,
+                    const double* group_uhg, const int32_t* group_len, const int32_t* group_river, size_t n_rivers,
+                    const double* river_uhg, const int32_t* river_len, const int32_t* river_downstream, size_t max_len,
+                    double* local, double* upstream, double* output, int dst_on_device) {
+    if (!group_sums || !group_uhg || !group_len || !group_river || !river_uhg || !river_len || !river_downstream ||
+        !local || !upstream || !output)
+        return fail(nullptr, "shyft_hip_route: null argument");
+    try {
+        if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
+        hip_check(hipSetDevice(device), "hipSetDevice");
+        const size_t R = n_rivers, G = n_groups;
+        if (R == 0 || T == 0) return 0;
+        if (max_len == 0) throw std::runtime_error("route: max_len == 0");
+        for (size_t g = 0; g < G; ++g) {
+            if (group_river[g] < 0 || size_t(group_river[g]) >= R) throw std::runtime_error("route: group river out of range");
+            if (group_len[g] < 1 || size_t(group_len[g]) > max_len) throw std::runtime_error("route: group UHG length");
+        }
+        // river CSR tables: groups of each river (ascending g), upstream rivers (ascending index = ascending id)
+        std::vector<int32_t> gro(R + 1, 0), grs(G), upo(R + 1, 0), ups;
+        for (size_t g = 0; g < G; ++g) gro[size_t(group_river[g]) + 1]++;
+        for (size_t r = 0; r < R; ++r) gro[r + 1] += gro[r];
+        {
+            std::vector<int32_t> pos(gro.begin(), gro.end() - 1);
+            for (size_t g = 0; g < G; ++g) grs[size_t(pos[size_t(group_river[g])]++)] = int32_t(g);
+        }
+        for (size_t r = 0; r < R; ++r) {
+            if (river_len[r] < 1 || size_t(river_len[r]) > max_len) throw std::runtime_error("route: river UHG length");
+            if (river_downstream[r] >= int32_t(R) || river_downstream[r] == int32_t(r))
+                throw std::runtime_error("route: invalid downstream river");
+        }
+        for (size_t r = 0; r < R; ++r) {
+            for (size_t u = 0; u < R; ++u)
+                if (river_downstream[u] == int32_t(r)) ups.push_back(int32_t(u));
+            upo[r + 1] = int32_t(ups.size());
+        }
+        // network levels: level(r) = 1 + max level of its upstream rivers (sources are level 0)
+        std::vector<int32_t> level(R, -1);
+        for (size_t pass = 0; pass <= R; ++pass) {
+            bool changed = false;
+            for (size_t r = 0; r < R; ++r) {
+                int32_t lv = 0;
+                bool ready = true;
+                for (int32_t k = upo[r]; k < upo[r + 1]; ++k) {
+                    if (level[size_t(ups[size_t(k)])] < 0) { ready = false; break; }
+                    lv = std::max(lv, level[size_t(ups[size_t(k)])] + 1);
+                }
+                if (ready && level[r] != lv) { level[r] = lv; changed = true; }
+            }
+            if (!changed) break;
+        }
+        int32_t n_levels = 0;
+        for (size_t r = 0; r < R; ++r) {
+            if (level[r] < 0) throw std::runtime_error("adding this river caused circular reference");
+            n_levels = std::max(n_levels, level[r] + 1);
+        }
+        std::vector<int32_t> lvl_off(size_t(n_levels) + 1, 0), lvl_rivers;
+        for (int32_t l = 0; l < n_levels; ++l) {
+            for (size_t r = 0; r < R; ++r)
+                if (level[r] == l) lvl_rivers.push_back(int32_t(r));
+            lvl_off[size_t(l) + 1] = int32_t(lvl_rivers.size());
+        }
+        hipStream_t s = nullptr;
+        hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+        struct stream_guard { hipStream_t s; ~stream_guard() { (void)hipStreamDestroy(s); } } sg{s};
+        dbuf<double> d_sums, d_gw, d_rw, d_local, d_up, d_in, d_out;
+        dbuf<int32_t> d_glen, d_gro, d_grs, d_rlen, d_upo, d_ups, d_lvl;
+        auto up_d = [&](dbuf<double>& b, const double* src, size_t n, int on_dev) {
+            b.alloc(std::max<size_t>(1, n));
+            if (n) hip_check(hipMemcpy(b.p, src, n * sizeof(double), on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice), "upload");
+        };
+        auto up_i = [&](dbuf<int32_t>& b, const int32_t* src, size_t n) {
+            b.alloc(std::max<size_t>(1, n));
+            if (n) hip_check(hipMemcpy(b.p, src, n * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
+        };
+        up_d(d_sums, group_sums, G * T, src_on_device);
+        up_d(d_gw, group_uhg, G * max_len, 0);
+        up_d(d_rw, river_uhg, R * max_len, 0);
+        up_i(d_glen, group_len, G);
+        up_i(d_gro, gro.data(), gro.size());
+        up_i(d_grs, grs.data(), grs.size());
+        up_i(d_rlen, river_len, R);
+        up_i(d_upo, upo.data(), upo.size());
+        up_i(d_ups, ups.data(), ups.size());
+        up_i(d_lvl, lvl_rivers.data(), lvl_rivers.size());
+        double* o_local = local;
+        double* o_up = upstream;
+        double* o_out = output;
+        if (!dst_on_device) {
+            d_local.alloc(R * T); d_up.alloc(R * T); d_out.alloc(R * T);
+            o_local = d_local.p; o_up = d_up.p; o_out = d_out.p;
+        }
+        d_in.alloc(R * T);
+        routing_args a;
+        a.n_steps = int(T);
+        a.n_rivers = int(R);
+        a.max_len = int(max_len);
+        a.group_sums = d_sums.p; a.group_w = d_gw.p; a.group_len = d_glen.p;
+        a.river_group_off = d_gro.p; a.river_groups = d_grs.p;
+        a.river_w = d_rw.p; a.river_len = d_rlen.p;
+        a.river_up_off = d_upo.p; a.river_up = d_ups.p; a.level_rivers = d_lvl.p;
+        a.local = o_local; a.upstream = o_up; a.inflow = d_in.p; a.output = o_out;
+        hip_check(launch_route(a, lvl_off.data(), n_levels, s), "route");
+        hip_check(hipStreamSynchronize(s), "route sync");
+        if (!dst_on_device) {
+            hip_check(hipMemcpy(local, o_local, R * T * sizeof(double), hipMemcpyDeviceToHost), "download");
+            hip_check(hipMemcpy(upstream, o_up, R * T * sizeof(double), hipMemcpyDeviceToHost), "download");
+            hip_check(hipMemcpy(output, o_out, R * T * sizeof(double), hipMemcpyDeviceToHost), "download");
+        }
+    } catch (const std::exception& e) {
+        return fail(nullptr, e.what());
+    }
+    return 0;
 }
 
 }  // extern "C"

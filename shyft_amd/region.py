@@ -172,3 +172,48 @@ class HipRegion:
 
     def catchment_sums_device(self, series: int, step0: int, n: int, dev_ptr: int):
         self._chk(self._L.shyft_hip_catchment_sums(self.h, series, step0, n, C.c_void_p(dev_ptr), 1))
+
+    # routing (routing.h:239-421): cells sharing (river, UHG) are one group
+    def set_routing_groups(self, group_of_cell, n_groups: int):
+        g = np.ascontiguousarray(group_of_cell, dtype=np.int32)
+        assert g.size == self.n
+        self._chk(self._L.shyft_hip_set_routing_groups(self.h, _ptr(g), int(n_groups)))
+        self.n_route_groups = int(n_groups)
+
+    def routing_group_sums(self, step0: int, n: int) -> np.ndarray:
+        out = np.empty((self.n_route_groups, n), dtype=np.float64)
+        self._chk(self._L.shyft_hip_routing_group_sums(self.h, step0, n, _ptr(out), 0))
+        return out
+
+    def routing_group_sums_device(self, step0: int, n: int, dev_ptr: int):
+        self._chk(self._L.shyft_hip_routing_group_sums(self.h, step0, n, C.c_void_p(dev_ptr), 1))
+
+
+def route(group_sums, group_uhgs, group_river, river_uhgs, river_downstream, device: int = -1, sums_dev_ptr=None,
+          T: int | None = None):
+    """River network evaluation on the device (shyft_hip_route). group_sums [G][T] (numpy) or sums_dev_ptr (+T);
+    group_uhgs / river_uhgs: lists of UHG weight vectors; group_river[G] and river_downstream[R] are river
+    indices (ascending river id), -1 = no downstream. Returns (local, upstream, output), each [R][T]."""
+    L = lib()
+    G, R = len(group_uhgs), len(river_uhgs)
+    max_len = max([1] + [len(w) for w in group_uhgs] + [len(w) for w in river_uhgs])
+    gw = np.zeros((G, max_len))
+    for k, w in enumerate(group_uhgs):
+        gw[k, :len(w)] = w
+    rw = np.zeros((R, max_len))
+    for k, w in enumerate(river_uhgs):
+        rw[k, :len(w)] = w
+    glen = np.array([len(w) for w in group_uhgs], dtype=np.int32)
+    rlen = np.array([len(w) for w in river_uhgs], dtype=np.int32)
+    gr = np.ascontiguousarray(group_river, dtype=np.int32)
+    rd = np.ascontiguousarray(river_downstream, dtype=np.int32)
+    if sums_dev_ptr is None:
+        s = np.ascontiguousarray(group_sums, dtype=np.float64)
+        T = s.shape[1]
+        src, on_dev = _ptr(s), 0
+    else:
+        src, on_dev = C.c_void_p(sums_dev_ptr), 1
+    out = [np.empty((R, T)) for _ in range(3)]
+    check(L.shyft_hip_route(device, G, T, src, on_dev, _ptr(gw), _ptr(glen), _ptr(gr), R, _ptr(rw), _ptr(rlen),
+                            _ptr(rd), max_len, _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), 0), None)
+    return tuple(out)

@@ -82,8 +82,42 @@ def load(variant: str = "detmath"):
     L.oracle_skaugen_sca_rel_red.argtypes = [C.c_uint64, C.c_uint64, _d, _d]
     L.oracle_ptssk_run.restype = C.c_int
     L.oracle_ptssk_run.argtypes = L.oracle_ptgsk_run.argtypes
+    L.oracle_route.restype = C.c_int
+    L.oracle_route.argtypes = [C.c_size_t, C.c_size_t, C.c_int64] + [C.c_void_p] * 4 + [C.c_size_t] + \
+        [C.c_void_p] * 4 + [C.c_int64] + [C.c_void_p] * 3
+    L.oracle_make_uhg.restype = None
+    L.oracle_make_uhg.argtypes = [C.c_int, _d, _d, C.c_void_p, C.POINTER(C.c_int)]
     _CACHE[variant] = L
     return L
+
+
+def route(q, dt_us, cell_rid, cell_dist, cell_vab, rivers, query, variant="detmath"):
+    """routing::model (routing.h:347-387) on the oracle. q [T][N] avg_discharge; rivers: list of
+    (id, downstream_id, distance, velocity, alpha, beta). Returns local, upstream, output [T]."""
+    L = load(variant)
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    T, N = q.shape
+    crid = np.ascontiguousarray(cell_rid, dtype=np.int64)
+    cd = np.ascontiguousarray(cell_dist, dtype=np.float64)
+    cv = np.ascontiguousarray(cell_vab, dtype=np.float64).reshape(N, 3)
+    rv = np.asarray(rivers, dtype=np.float64).reshape(-1, 6)
+    rid = np.ascontiguousarray(rv[:, 0], dtype=np.int64)
+    ds = np.ascontiguousarray(rv[:, 1], dtype=np.int64)
+    rd = np.ascontiguousarray(rv[:, 2])
+    rvab = np.ascontiguousarray(rv[:, 3:6])
+    out = [np.empty(T) for _ in range(3)]
+    if L.oracle_route(N, T, int(dt_us), _p(q), _p(crid), _p(cd), _p(cv), len(rid), _p(rid), _p(ds), _p(rd), _p(rvab),
+                      int(query), _p(out[0]), _p(out[1]), _p(out[2])) != 0:
+        raise RuntimeError("oracle_route failed")
+    return tuple(out)
+
+
+def make_uhg(n_steps, alpha, beta, variant="detmath"):
+    L = load(variant)
+    buf = np.empty(max(1, n_steps))
+    n = C.c_int(0)
+    L.oracle_make_uhg(int(n_steps), float(alpha), float(beta), _p(buf), C.byref(n))
+    return buf[:n.value].copy()
 
 
 SKAUGEN_DEFAULT = (40.77, 113.0, 0.1, 0.1, 0.16, 2.5, 0.14, 0.01)  # skaugen::parameter() (skaugen.h:89-112)
