@@ -50,6 +50,7 @@ STACKS = {
     #        kernel name)
     "pt_gs_k": (40, 16, 2 * 9 * 8, "ptgsk_run_kernel"),      # T P WS RH RAD in; discharge, charge out; 9 state
     "hbv_stack": (32, 16, 2 * 22 * 8, "hbv_run_kernel"),     # wind not read (hbv_stack.h:295-301); 22 state
+    "pt_ss_k": (40, 16, 2 * 8 * 8, "ptssk_run_kernel"),      # T P WS RH RAD in (WS unused by skaugen); 8 state
 }
 
 
@@ -60,7 +61,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=0,
                     help="cells per GPU (default 1,048,576 for pt_gs_k, 524,288 for hbv_stack)")
-    ap.add_argument("--stack", choices=("pt_gs_k", "hbv_stack"), default="pt_gs_k")
+    ap.add_argument("--stack", choices=("pt_gs_k", "hbv_stack", "pt_ss_k"), default="pt_gs_k")
+    ap.add_argument("--routing", action="store_true",
+                    help="configs[4]: route avg_discharge through the synthetic river network (routing::uhg): "
+                         "per chunk the (river, UHG)-group sums are formed on each GPU and all-gathered, after the "
+                         "last chunk the network is convolved on the device (on by default for --stack pt_ss_k)")
+    ap.add_argument("--no-routing", action="store_true")
     ap.add_argument("--chunk", type=int, default=CHUNK)
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
@@ -142,13 +148,16 @@ def stack_defaults(stack, cells):
     from shyft_amd import synthetic
     if stack == "hbv_stack":
         return synthetic.default_hbv_parameters(), synthetic.default_hbv_state(cells)
+    if stack == "pt_ss_k":
+        return synthetic.default_ptssk_parameters(), synthetic.default_ptssk_state(cells)
     return synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(cells)
 
 
 def build_region(stack, cells, world, rank, local, chunk, n_steps_axis):
     from shyft_amd import synthetic
-    from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, COLLECT_DISCHARGE
-    r = HipRegion(HBV_STACK if stack == "hbv_stack" else PT_GS_K, cells, device=local)
+    from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, PT_SS_K, COLLECT_DISCHARGE
+    sid = {"pt_gs_k": PT_GS_K, "hbv_stack": HBV_STACK, "pt_ss_k": PT_SS_K}[stack]
+    r = HipRegion(sid, cells, device=local)
     r.set_geo(synthetic.geo11(cells, n_catchments=100 * world, cell_offset=rank * cells, n_total=world * cells))
     r.set_parameters(stack_defaults(stack, 1)[0])
     r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, n_steps_axis, chunk)
@@ -156,9 +165,54 @@ def build_region(stack, cells, world, rank, local, chunk, n_steps_axis):
     return r
 
 
-def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None):
+class Router:
+    """configs[4] routing (core/routing.h:239-421) over the synthetic river network of the whole region:
+    per chunk each rank reduces its cells' avg_discharge to the global (river, UHG) group sums on its GPU and
+    the partials are all-gathered and added in rank order (RCCL over xGMI); after the last chunk every rank
+    convolves the network on its device (shyft_hip_route)."""
+
+    def __init__(self, r, cells, world, rank, local, n_axis, pg):
+        import torch
+        from shyft_amd import api, synthetic
+        self.n_catch = 100 * world
+        _, _, group = synthetic.cell_routing(cells, self.n_catch, cell_offset=rank * cells, n_total=world * cells)
+        self.G = self.n_catch * len(synthetic.ROUTE_DISTANCES)
+        r.set_routing_groups(group, self.G)
+        self.rivers = synthetic.river_network(self.n_catch)
+        steps = [int((d / 1.0) / 3600.0 + 0.5) for d in synthetic.ROUTE_DISTANCES]
+        self.group_uhgs = [api.make_uhg_from_gamma(steps[k], 7.0, 0.0) for _ in range(self.n_catch)
+                           for k in range(len(steps))]
+        self.group_river = [g // len(steps) for g in range(self.G)]
+        self.river_uhgs = [api.make_uhg_from_gamma(int((d / v) / 3600.0 + 0.5), a, b) for (_, _, d, v, a, b) in self.rivers]
+        self.river_down = [ds - 1 for (_, ds, *_rest) in self.rivers]
+        self.dev = torch.device("cuda", local)
+        self.sums = torch.zeros((self.G, n_axis), dtype=torch.float64, device=self.dev)
+        self.part = None
+        self.pg = pg
+        self.out = None
+
+    def chunk(self, r, step0, n):
+        import torch
+        from shyft_amd import distributed
+        if self.part is None or self.part.shape[1] != n:
+            self.part = torch.empty((self.G, n), dtype=torch.float64, device=self.dev)
+        torch.cuda.synchronize(self.dev)
+        r.routing_group_sums_device(step0, n, self.part.data_ptr())
+        self.sums[:, step0:step0 + n] = distributed.combine_partials(self.part)
+
+    def finish(self, T):
+        import torch
+        from shyft_amd.region import route
+        s = self.sums[:, :T].contiguous()
+        torch.cuda.synchronize(self.dev)
+        self.out = route(None, self.group_uhgs, self.group_river, self.river_uhgs, self.river_down,
+                         device=self.dev.index, sums_dev_ptr=s.data_ptr(), T=T)
+        return self.out
+
+
+def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
-    or IDW from the station network), then run_cells."""
+    or IDW from the station network), then run_cells (and the routing group sums)."""
     kernel_ms = []
     r.set_state(state0)
     for s in range(k_steps):
@@ -173,6 +227,10 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None):
                 r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
         r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
+        if router is not None:
+            router.chunk(r, step0, chunk)
+    if router is not None:
+        router.finish(k_steps * chunk)
     return kernel_ms
 
 
@@ -181,7 +239,7 @@ def cpu_baseline(stack, n_cells, threads):
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K
     from tests import oracle_lib
-    run = oracle_lib.hbv_run if stack == "hbv_stack" else oracle_lib.ptgsk_run
+    run = {"hbv_stack": oracle_lib.hbv_run, "pt_ss_k": oracle_lib.ptssk_run}.get(stack, oracle_lib.ptgsk_run)
     # forcing of the sample cells: identical bits from the device generator (tests/test_capi.py pins equality)
     g = HipRegion(PT_GS_K, n_cells, device=0)
     g.set_geo(synthetic.geo11(n_cells, n_total=1 << 20))
@@ -254,12 +312,15 @@ def main():
         xyz = station_network(world * cells)
         stations = (xyz, [station_values(xyz, s * chunk, chunk) for s in range(max(a.steps, a.warmup))])
 
+    routing = (a.routing or a.stack == "pt_ss_k") and not a.no_routing
+    router = Router(r, cells, world, rank, local, n_axis, pg) if routing else None
+
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
-        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations)
+        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations, router)
     barrier_sync(pg, local)
     t0 = time.perf_counter()
-    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations)
+    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations, router)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
@@ -288,7 +349,7 @@ def main():
             "workload": (f"{a.stack} + inverse_distance from {N_STATIONS} stations, " if a.idw else f"{a.stack} ") +
                         f"region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
                         f"({a.steps} chunks of {chunk}), discharge_collector, default "
-                        f"{'HbvParameter' if a.stack == 'hbv_stack' else 'PTGSKParameter'}",
+                        f"{dict(hbv_stack='HbvParameter', pt_ss_k='PTSSKParameter').get(a.stack, 'PTGSKParameter')}",
             "cells_per_gpu": cells,
             "total_cells": world * cells,
             "steps_per_chunk": chunk,
@@ -312,6 +373,13 @@ def main():
                     f"{state_b} B/cell state per launch (DESIGN.md)",
         },
     }
+    if router is not None:
+        o = router.out[2]
+        out["config"]["workload"] += (f"; routing::uhg through a {len(router.rivers)}-river network "
+                                      f"({router.G} (river, UHG) groups all-gathered per chunk, network convolved on "
+                                      f"device after the last chunk)")
+        out["routing"] = {"rivers": len(router.rivers), "groups": router.G,
+                          "outlet_mean_m3s": float(o[0].mean()), "outlet_max_m3s": float(o[0].max())}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         out["cpu_baseline"] = cpu_baseline(a.stack, a.cpu_cells, threads)

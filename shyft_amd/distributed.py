@@ -54,6 +54,23 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
     return float(t.item())
 
 
+def routing_group_sums(region, local_groups, n_global_groups: int, step0: int, n: int, group=None, device=None):
+    """Discharge sums of the global routing groups (cells sharing river + UHG, core/routing.h:326-345) over
+    ALL ranks' cells. local_groups[n_local_cells] holds each local cell's global group index (-1 = not
+    routed); the rank's group sums are formed on its GPU and combined in rank order (combine_partials).
+    Returns a torch tensor [n_global_groups][n] on `device`, identical on every rank."""
+    import torch
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    region.set_routing_groups(local_groups, n_global_groups)
+    part = torch.empty((n_global_groups, n), dtype=torch.float64, device=dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+        region.routing_group_sums_device(step0, n, part.data_ptr())
+    else:
+        part.copy_(torch.from_numpy(region.routing_group_sums(step0, n)))
+    return combine_partials(part, group)
+
+
 def catchment_sums(region, series: int, step0: int, n: int, global_cids, group=None, device=None):
     """Per-catchment sums of a response series over ALL ranks' cells.
 

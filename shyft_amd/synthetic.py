@@ -160,6 +160,31 @@ def default_ptssk_parameters() -> np.ndarray:
 PTSSK_NS = 8  # nu alpha sca swe free_water residual num_units kirchner.q
 
 
+# ---- synthetic river network for configs[4] (pt_ss_k + routing::uhg) --------------------------------------------------
+# One river per catchment (river id = catchment id). River k drains into river k // 2 (a binary tree rooted at
+# river 1), 4 km + 1 km*(k % 7) downstream, UHGParameter() defaults (velocity 1 m/s, alpha 7, beta 0,
+# routing.h:70-76). Each cell routes to its catchment's river at 0 m or 7200 m (a 2-step cell UHG at the
+# default routing velocity), chosen by the cell hash; cells sharing (river, distance class) are one routing group.
+ROUTE_DISTANCES = (0.0, 7200.0)
+
+
+def river_network(n_rivers: int):
+    """[(id, downstream_id, distance, velocity, alpha, beta)] for rivers 1..n_rivers."""
+    return [(k, k // 2, 4000.0 + 1000.0 * (k % 7), 1.0, 7.0, 0.0) for k in range(1, n_rivers + 1)]
+
+
+def cell_routing(n_cells: int, n_catchments: int, seed: int = SEED, cell_offset: int = 0, n_total: int | None = None):
+    """(river id [n], routing distance [n], global routing group [n]) of cells [cell_offset, cell_offset+n)."""
+    n_total = n_total or (cell_offset + n_cells)
+    i = np.arange(cell_offset, cell_offset + n_cells, dtype=np.int64)
+    rid = 1 + (i * n_catchments) // n_total
+    cells = np.arange(cell_offset, cell_offset + n_cells, dtype=np.uint64)
+    klass = (_u(_key(seed, cells, np.zeros_like(cells)), 11) < 0.5).astype(np.int64)
+    dist = np.asarray(ROUTE_DISTANCES)[klass]
+    group = (rid - 1) * len(ROUTE_DISTANCES) + klass
+    return rid, dist, group.astype(np.int32)
+
+
 def default_ptssk_state(n_cells: int, q: float = 1.0) -> np.ndarray:
     """PTSSKState(): skaugen::state() (skaugen.h:122-124: nu 4.077, alpha 40.77, no snow) with kirchner.q = q."""
     s = np.zeros((n_cells, PTSSK_NS), dtype=np.float64)

@@ -52,6 +52,61 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+class _FakeRegion:
+    """CPU stand-in for HipRegion's routing-group interface (the per-rank device reduction)."""
+
+    def __init__(self, q):
+        self.q = q  # [T][n_local]
+
+    def set_routing_groups(self, group_of_cell, n_groups):
+        self.g, self.G = np.asarray(group_of_cell), n_groups
+
+    def routing_group_sums(self, step0, n):
+        out = np.zeros((self.G, n))
+        for c in range(self.q.shape[1]):
+            if self.g[c] >= 0:
+                out[self.g[c]] += self.q[step0:step0 + n, c]
+        return out
+
+
+def _routing_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shyft_amd import synthetic
+        n_total, T, C = 64, 12, 4
+        series = np.random.default_rng(1).random((T, n_total))
+        b, e = distributed.shard_range(n_total, world, rank)
+        _, _, group = synthetic.cell_routing(e - b, C, cell_offset=b, n_total=n_total)
+        sums = distributed.routing_group_sums(_FakeRegion(series[:, b:e]), group, C * 2, 0, T,
+                                              device=torch.device("cpu")).numpy()
+        q.put((rank, sums))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_routing_group_sums_gloo_world2():
+    """Global (river, UHG) group sums from sharded cells equal the unsharded sums, identically on every rank."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_routing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][1], res[1][1])
+    from shyft_amd import synthetic
+    n_total, T, C = 64, 12, 4
+    series = np.random.default_rng(1).random((T, n_total))
+    _, _, group = synthetic.cell_routing(n_total, C, n_total=n_total)
+    ref = np.stack([series[:, group == g].sum(axis=1) for g in range(2 * C)])
+    assert np.allclose(res[0][1], ref, rtol=1e-13, atol=1e-14)
+
+
 def test_combine_partials_gloo_world2():
     world = 2
     port = _free_port()
