@@ -217,7 +217,9 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router
     r.set_state(state0)
     for s in range(k_steps):
         step0 = s * chunk
-        r.set_window(step0)
+        # the chunk's forcing rows are all rewritten below and run_cells writes every response row of the
+        # window, so the window moves without the NaN pre-fill of set_window
+        r.move_window(step0, 0)
         if stations is None:
             r.synthetic_forcing(seed, step0, chunk, cell_offset=rank * cells)
         else:

@@ -87,6 +87,10 @@ int shyft_hip_set_time_axis(shyft_hip_region* h, int64_t t0_us, int64_t dt_us, s
 /* Move the resident window to start at step w0 (window length unchanged). Forcing
  * in the window becomes NaN, responses NaN. Used to stream long horizons in chunks. */
 int shyft_hip_set_window(shyft_hip_region* h, size_t w0);
+/* set_window with control over the NaN fill: fill_mask bit 0 forcing, bit 1 responses, bit 2 state series
+ * (set_window == fill_mask 7). A caller that rewrites the whole window (a device forcing generator, a full
+ * run_cells over the window) passes 0 and saves a pass over the window's HBM. */
+int shyft_hip_move_window(shyft_hip_region* h, size_t w0, int fill_mask);
 
 /* Collection mode (shyft_hip_collect) and state collection on/off
  * (set_state_collection / set_snow_sca_swe_collection, region_model.h:784-818). */

@@ -29,6 +29,7 @@ SIGNATURES = {
     "shyft_hip_set_parameters": (C.c_int, [_h, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]),
     "shyft_hip_set_time_axis": (C.c_int, [_h, C.c_int64, C.c_int64, C.c_size_t, C.c_size_t]),
     "shyft_hip_set_window": (C.c_int, [_h, C.c_size_t]),
+    "shyft_hip_move_window": (C.c_int, [_h, C.c_size_t, C.c_int]),
     "shyft_hip_set_collection": (C.c_int, [_h, C.c_int, C.c_int]),
     "shyft_hip_set_catchment_filter": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_set_state": (C.c_int, [_h, C.c_void_p, C.c_size_t]),

@@ -126,6 +126,7 @@ struct idw_gather_args {
     double default_gradient;
     const double* src_xyz;     // [S][3]
     const double* src_values;  // [n_rows][S]
+    const double* dst_xyz;     // [N][3] cell mid points (temperature: d.z - s.z)
     const double* slope;       // [N] radiation slope factor (geo_cell_data)
     const int32_t* idx;
     const double* w;

@@ -91,118 +91,236 @@ __global__ __launch_bounds__(128) void idw_neighbours_kernel(idw_nb_args a) {
     }
 }
 
-// The lane's neighbour list (source index, weight, transform constant and the
-// source z for the gradient) is loaded ONCE into registers (KT >= count, a
-// compile-time bound so the arrays stay in VGPRs) and reused for every row; only
-// the [row][source] values (a few KB per row, L1/L2 resident) are gathered per step.
-template <int KT>
-__global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= a.n_cells) return;
-    if (a.active && !a.active[j]) return;
+// Per lane (cell) the neighbour list -- source index and weight, plus the
+// precipitation factor pow(scale, dz/100) -- is loaded ONCE into registers and
+// reused for every row. The [row][source] values are staged through LDS a tile
+// of rows at a time (loaded cooperatively, coalesced), together with the source
+// coordinates, so a neighbour lookup is an LDS read instead of a scattered
+// 8-byte L2 gather, and the temperature transform's d.z - s.z is formed from the
+// LDS copy of s.z (the expression the neighbour kernel evaluates, so the bits are
+// the same). The kernel is specialised on the model (KIND) and on
+// gradient_by_equation so each variant keeps only the registers it needs
+// (occupancy). The temperature gradient pass re-reads the LDS row instead of
+// holding the K values in registers. When the source table is too large for the
+// LDS budget the rows and coordinates are read from global memory (LDS = false).
+template <int KT, int KIND, bool BYEQ, bool LDS>
+__device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lane_on, double* smem, int lds_rows) {
     const size_t N = (size_t)a.n_cells;
-    const int kept = a.count[j];
+    if (!lane_on) j = 0;  // an idle lane still joins the tile loads, computes on cell 0 and stores nothing
     const int S = a.n_sources;
-    const double slope = a.slope ? a.slope[j] : 0.9;
-    const bool temp = a.kind == IDW_TEMPERATURE;
+    const int kept = a.count[j];
+    const double slope = KIND == IDW_RADIATION ? (a.slope ? a.slope[j] : 0.9) : 0.0;
+    // LDS layout: [src x | src y | src z] (temperature only) then the row tile
+    double* sxyz = smem;
+    double* tile = smem + (KIND == IDW_TEMPERATURE ? 3 * S : 0);
+    if (LDS && KIND == IDW_TEMPERATURE) {
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            sxyz[i] = a.src_xyz[3 * i];
+            sxyz[S + i] = a.src_xyz[3 * i + 1];
+            sxyz[2 * S + i] = a.src_xyz[3 * i + 2];
+        }
+    }
+    auto src_x = [&](int s) { return LDS ? sxyz[s] : a.src_xyz[3 * s]; };
+    auto src_y = [&](int s) { return LDS ? sxyz[S + s] : a.src_xyz[3 * s + 1]; };
+    auto src_z = [&](int s) { return LDS ? sxyz[2 * S + s] : a.src_xyz[3 * s + 2]; };
+    const double dst_z = KIND == IDW_TEMPERATURE ? a.dst_xyz[3 * (size_t)j + 2] : 0.0;
     int nidx[KT];
-    double nw[KT], naux[KT], nx[KT], ny[KT], nz[KT];
+    double nw[KT];
+    double naux[KIND == IDW_PRECIPITATION ? KT : 1];
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
         const bool in = k < kept;
-        const int s = in ? a.idx[k * N + j] : 0;
-        nidx[k] = s;
+        nidx[k] = in ? a.idx[k * N + j] : 0;
         nw[k] = in ? a.w[k * N + j] : 0.0;
-        naux[k] = in ? a.aux[k * N + j] : 0.0;
-        nz[k] = (in && temp) ? a.src_xyz[3 * s + 2] : 0.0;
-        nx[k] = (in && temp && a.by_equation) ? a.src_xyz[3 * s] : 0.0;
-        ny[k] = (in && temp && a.by_equation) ? a.src_xyz[3 * s + 1] : 0.0;
+        if (KIND == IDW_PRECIPITATION) naux[k] = in ? a.aux[k * N + j] : 0.0;
     }
     double* __restrict__ out = a.out;
-    for (int r = 0; r < a.n_rows; ++r) {
-        const double* __restrict__ row = a.src_values + (size_t)r * S;
-        double v[KT];
+    // Temperature fast path: when every source value of a row is finite (the common case) the gradient
+    // scan's outcome depends only on the neighbours' fixed geometry -- which neighbour holds the lowest and
+    // the highest z, and (gradient_by_equation) the 3x3 system of the first four neighbours. Both are
+    // resolved once per lane here with the scan's own comparisons and expressions; a row with a non-finite
+    // source takes the general scan below. Results are bit-identical either way.
+    __shared__ int row_finite[64];
+    int kmin = 0, kmax = 0;
+    double inv[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    bool inv_ok = false;
+    if (KIND == IDW_TEMPERATURE && LDS) {
+        __syncthreads();  // coordinates stored
+        double z_mn = 0, z_mx = 0;
 #pragma unroll
-        for (int k = 0; k < KT; ++k) v[k] = k < kept ? row[nidx[k]] : 0.0;
-        double scale = 1.0;
-        if (temp) {
-            // temperature_gradient_scale_computer::compute over the valid neighbours in
-            // neighbour order (inverse_distance.h:305-330)
-            int n = 0;
-            double z_mn = 0, z_mx = 0, t_mn = 0, t_mx = 0;
-            double p0x = 0, p0y = 0, p0z = 0, t0 = 0;
-            double A[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, b[3] = {0, 0, 0};
+        for (int k = 0; k < KT; ++k) {
+            if (k >= kept) continue;
+            const double sz = src_z(nidx[k]);
+            if (k == 0) { z_mn = z_mx = sz; kmin = kmax = 0; }
+            else if (sz < z_mn) { z_mn = sz; kmin = k; }
+            else if (sz > z_mx) { z_mx = sz; kmax = k; }
+        }
+        if (BYEQ && kept > 3) {
+            double A[3][3];
+            const double p0x = src_x(nidx[0]), p0y = src_y(nidx[0]), p0z = src_z(nidx[0]);
 #pragma unroll
-            for (int k = 0; k < KT; ++k) {
-                if (k >= kept || !__builtin_isfinite(v[k])) continue;
-                const double sz = nz[k];
-                if (n == 0) {
-                    z_mn = z_mx = sz;
-                    t_mn = t_mx = v[k];
-                } else if (sz < z_mn) {
-                    z_mn = sz; t_mn = v[k];
-                } else if (sz > z_mx) {
-                    z_mx = sz; t_mx = v[k];
-                }
-                if (a.by_equation) {
-                    if (n == 0) { p0x = nx[k]; p0y = ny[k]; p0z = sz; t0 = v[k]; }
-                    else if (n == 1) { A[0][0] = nx[k] - p0x; A[0][1] = ny[k] - p0y; A[0][2] = sz - p0z; b[0] = v[k] - t0; }
-                    else if (n == 2) { A[1][0] = nx[k] - p0x; A[1][1] = ny[k] - p0y; A[1][2] = sz - p0z; b[1] = v[k] - t0; }
-                    else if (n == 3) { A[2][0] = nx[k] - p0x; A[2][1] = ny[k] - p0y; A[2][2] = sz - p0z; b[2] = v[k] - t0; }
-                }
-                ++n;
+            for (int q = 0; q < 3; ++q) {
+                A[q][0] = src_x(nidx[q + 1]) - p0x; A[q][1] = src_y(nidx[q + 1]) - p0y; A[q][2] = src_z(nidx[q + 1]) - p0z;
             }
-            bool solved = false;
-            if (a.by_equation && n > 3) {
-                // arma::solve on the 3x3 system of the first four valid points: determinant + cofactors
-                const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) -
-                                   A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
-                                   A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
-                if (fabs(det) > 0.0 && __builtin_isfinite(det)) {
-                    const double i00 = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
-                    const double i01 = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
-                    const double i02 = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
-                    const double i10 = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
-                    const double i11 = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
-                    const double i12 = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
-                    const double i20 = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
-                    const double i21 = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
-                    const double i22 = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
-                    const double x0 = i00 * b[0] + i01 * b[1] + i02 * b[2];
-                    const double x1 = i10 * b[0] + i11 * b[1] + i12 * b[2];
-                    const double x2 = i20 * b[0] + i21 * b[1] + i22 * b[2];
+            const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) -
+                               A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                               A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+            if (fabs(det) > 0.0 && __builtin_isfinite(det)) {
+                inv_ok = true;
+                inv[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+                inv[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+                inv[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+                inv[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+                inv[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+                inv[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+                inv[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+                inv[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+                inv[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+            }
+        }
+    }
+    const int step = LDS ? lds_rows : a.n_rows;
+    for (int r0 = 0; r0 < a.n_rows; r0 += step) {
+        const int r1 = r0 + step < a.n_rows ? r0 + step : a.n_rows;
+        if (LDS) {
+            __syncthreads();  // the previous tile is consumed (and the coordinates are stored)
+            if (KIND == IDW_TEMPERATURE) {
+                if ((int)threadIdx.x < r1 - r0) row_finite[threadIdx.x] = 1;
+                __syncthreads();
+            }
+            const int n = (r1 - r0) * S;
+            const double* __restrict__ src = a.src_values + (size_t)r0 * S;
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const double v = src[i];
+                tile[i] = v;
+                if (KIND == IDW_TEMPERATURE && !__builtin_isfinite(v)) row_finite[i / S] = 0;
+            }
+            __syncthreads();
+        }
+        for (int r = r0; r < r1; ++r) {
+            const double* __restrict__ row = LDS ? tile + (size_t)(r - r0) * S : a.src_values + (size_t)r * S;
+            double scale = 1.0;
+            if (KIND == IDW_TEMPERATURE && LDS && row_finite[r - r0]) {
+                bool solved = false;
+                if (BYEQ && inv_ok) {
+                    const double t0 = row[nidx[0]];
+                    const double b0 = row[nidx[1]] - t0, b1 = row[nidx[2]] - t0, b2 = row[nidx[3]] - t0;
+                    const double x0 = inv[0][0] * b0 + inv[0][1] * b1 + inv[0][2] * b2;
+                    const double x1 = inv[1][0] * b0 + inv[1][1] * b1 + inv[1][2] * b2;
+                    const double x2 = inv[2][0] * b0 + inv[2][1] * b1 + inv[2][2] * b2;
                     if (__builtin_isfinite(x0) && __builtin_isfinite(x1) && __builtin_isfinite(x2)) {
                         scale = x2;
                         solved = true;
                     }
                 }
-            }
-            if (!solved) {
-                if (n > 1) {
-                    const double dzm = z_mx - z_mn;
-                    scale = dzm > 50.0 ? (t_mx - t_mn) / dzm : a.default_gradient;
-                } else {
-                    scale = a.default_gradient;
+                if (!solved) {
+                    if (kept > 1) {
+                        const double dzm = src_z(nidx[kmax]) - src_z(nidx[kmin]);
+                        scale = dzm > 50.0 ? (row[nidx[kmax]] - row[nidx[kmin]]) / dzm : a.default_gradient;
+                    } else {
+                        scale = a.default_gradient;
+                    }
+                }
+            } else if (KIND == IDW_TEMPERATURE) {
+                // temperature_gradient_scale_computer over the valid neighbours in neighbour order
+                // (inverse_distance.h:305-330)
+                int n = 0;
+                double z_mn = 0, z_mx = 0, t_mn = 0, t_mx = 0;
+                double p0x = 0, p0y = 0, p0z = 0, t0 = 0;
+                double A[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, b[3] = {0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < KT; ++k) {
+                    if (k >= kept) continue;
+                    const double v = row[nidx[k]];
+                    if (!__builtin_isfinite(v)) continue;
+                    const double sz = src_z(nidx[k]);
+                    if (n == 0) {
+                        z_mn = z_mx = sz;
+                        t_mn = t_mx = v;
+                    } else if (sz < z_mn) {
+                        z_mn = sz; t_mn = v;
+                    } else if (sz > z_mx) {
+                        z_mx = sz; t_mx = v;
+                    }
+                    if (BYEQ) {
+                        const double sx = src_x(nidx[k]), sy = src_y(nidx[k]);
+                        if (n == 0) { p0x = sx; p0y = sy; p0z = sz; t0 = v; }
+                        else if (n == 1) { A[0][0] = sx - p0x; A[0][1] = sy - p0y; A[0][2] = sz - p0z; b[0] = v - t0; }
+                        else if (n == 2) { A[1][0] = sx - p0x; A[1][1] = sy - p0y; A[1][2] = sz - p0z; b[1] = v - t0; }
+                        else if (n == 3) { A[2][0] = sx - p0x; A[2][1] = sy - p0y; A[2][2] = sz - p0z; b[2] = v - t0; }
+                    }
+                    ++n;
+                }
+                bool solved = false;
+                if (BYEQ && n > 3) {
+                    // arma::solve on the 3x3 system of the first four valid points: determinant + cofactors
+                    const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) -
+                                       A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                                       A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+                    if (fabs(det) > 0.0 && __builtin_isfinite(det)) {
+                        const double i20 = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+                        const double i21 = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+                        const double i22 = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+                        const double i00 = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+                        const double i01 = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+                        const double i02 = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+                        const double i10 = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+                        const double i11 = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+                        const double i12 = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+                        const double x0 = i00 * b[0] + i01 * b[1] + i02 * b[2];
+                        const double x1 = i10 * b[0] + i11 * b[1] + i12 * b[2];
+                        const double x2 = i20 * b[0] + i21 * b[1] + i22 * b[2];
+                        if (__builtin_isfinite(x0) && __builtin_isfinite(x1) && __builtin_isfinite(x2)) {
+                            scale = x2;
+                            solved = true;
+                        }
+                    }
+                }
+                if (!solved) {
+                    if (n > 1) {
+                        const double dzm = z_mx - z_mn;
+                        scale = dzm > 50.0 ? (t_mx - t_mn) / dzm : a.default_gradient;
+                    } else {
+                        scale = a.default_gradient;
+                    }
                 }
             }
-        }
-        double sum_weights = 0.0, sum_weight_value = 0.0;
+            double sum_weights = 0.0, sum_weight_value = 0.0;
+            // second pass over the row: hide the pointer from the optimiser so the K values of the gradient
+            // pass are re-read from LDS rather than kept live in VGPRs (occupancy)
+            const double* rowp = row;
+            if (KIND == IDW_TEMPERATURE && LDS) asm volatile("" : "+v"(rowp));
 #pragma unroll
-        for (int k = 0; k < KT; ++k) {
-            if (k >= kept || !__builtin_isfinite(v[k])) continue;
-            double tr;
-            switch (a.kind) {
-                case IDW_TEMPERATURE: tr = v[k] + scale * naux[k]; break;
-                case IDW_PRECIPITATION: tr = v[k] * naux[k]; break;
-                case IDW_RADIATION: tr = v[k] * slope; break;
-                default: tr = v[k]; break;
+            for (int k = 0; k < KT; ++k) {
+                if (k >= kept) continue;
+                const double v = rowp[nidx[k]];
+                if (!__builtin_isfinite(v)) continue;
+                double tr;
+                if (KIND == IDW_TEMPERATURE) tr = v + scale * (dst_z - src_z(nidx[k]));
+                else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
+                else if (KIND == IDW_RADIATION) tr = v * slope;
+                else tr = v;
+                sum_weight_value += nw[k] * tr;
+                sum_weights += nw[k];
             }
-            sum_weight_value += nw[k] * tr;
-            sum_weights += nw[k];
+            if (lane_on) out[(size_t)r * N + j] = sum_weight_value / sum_weights;
         }
-        out[(size_t)r * N + j] = sum_weight_value / sum_weights;
     }
 }
+
+template <int KT, int KIND, bool BYEQ>
+__global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a, int lds_rows) {
+    extern __shared__ double smem[];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool lane_on = j < a.n_cells && !(a.active && !a.active[j]);
+    if (lds_rows > 0) {
+        // every lane of the workgroup takes part in the tile loads and barriers
+        idw_gather_body<KT, KIND, BYEQ, true>(a, j, lane_on, smem, lds_rows);
+    } else if (lane_on) {
+        idw_gather_body<KT, KIND, BYEQ, false>(a, j, true, smem, 0);
+    }
+}
+
 
 // single temperature source: copied to every calculated cell (region_model.h:470-481)
 __global__ void copy_source_kernel(const double* __restrict__ v, int n_rows, int n_cells, const uint8_t* __restrict__ active,
@@ -224,11 +342,36 @@ hipError_t launch_idw_neighbours(const idw_nb_args& a, hipStream_t stream) {
 hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
     if (a.n_cells == 0 || a.n_rows == 0) return hipSuccess;
     const dim3 grid((a.n_cells + 255) / 256), block(256);
-    // smallest register-resident list that holds max_members
-    if (a.max_members <= 8) hipLaunchKernelGGL(idw_gather_kernel<8>, grid, block, 0, stream, a);
-    else if (a.max_members <= 12) hipLaunchKernelGGL(idw_gather_kernel<12>, grid, block, 0, stream, a);
-    else if (a.max_members <= 20) hipLaunchKernelGGL(idw_gather_kernel<20>, grid, block, 0, stream, a);
-    else hipLaunchKernelGGL(idw_gather_kernel<IDW_KMAX>, grid, block, 0, stream, a);
+    // LDS: the source coordinates (temperature) + a tile of source rows, up to 32 KB per workgroup
+    constexpr size_t LDS_BUDGET = 32 * 1024;
+    const size_t row_bytes = (size_t)a.n_sources * sizeof(double);
+    const size_t coord_bytes = a.kind == IDW_TEMPERATURE ? 3 * row_bytes : 0;
+    int lds_rows = row_bytes + coord_bytes <= LDS_BUDGET ? (int)((LDS_BUDGET - coord_bytes) / row_bytes) : 0;
+    if (lds_rows > 64) lds_rows = 64;  // row_finite[] flags per tile
+    if (lds_rows > a.n_rows) lds_rows = a.n_rows;
+    const size_t shm = lds_rows > 0 ? coord_bytes + (size_t)lds_rows * row_bytes : 0;
+    // smallest register-resident list that holds max_members, per model
+#define SHYFT_IDW_LAUNCH(KIND_, BYEQ_)                                                                               \
+    do {                                                                                                             \
+        if (a.max_members <= 8)                                                                                      \
+            hipLaunchKernelGGL((idw_gather_kernel<8, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);         \
+        else if (a.max_members <= 12)                                                                                \
+            hipLaunchKernelGGL((idw_gather_kernel<12, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);        \
+        else if (a.max_members <= 20)                                                                                \
+            hipLaunchKernelGGL((idw_gather_kernel<20, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);        \
+        else                                                                                                         \
+            hipLaunchKernelGGL((idw_gather_kernel<IDW_KMAX, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);  \
+    } while (0)
+    switch (a.kind) {
+        case IDW_TEMPERATURE:
+            if (a.by_equation) SHYFT_IDW_LAUNCH(IDW_TEMPERATURE, true);
+            else SHYFT_IDW_LAUNCH(IDW_TEMPERATURE, false);
+            break;
+        case IDW_PRECIPITATION: SHYFT_IDW_LAUNCH(IDW_PRECIPITATION, false); break;
+        case IDW_RADIATION: SHYFT_IDW_LAUNCH(IDW_RADIATION, false); break;
+        default: SHYFT_IDW_LAUNCH(IDW_WIND_SPEED, false); break;  // wind speed and rel_hum: plain mean
+    }
+#undef SHYFT_IDW_LAUNCH
     return hipGetLastError();
 }
 

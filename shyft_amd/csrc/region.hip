@@ -559,15 +559,18 @@ int shyft_hip_set_time_axis(shyft_hip_region* h, int64_t t0_us, int64_t dt_us, s
     });
 }
 
-int shyft_hip_set_window(shyft_hip_region* h, size_t w0) {
+int shyft_hip_set_window(shyft_hip_region* h, size_t w0) { return shyft_hip_move_window(h, w0, 7); }
+
+int shyft_hip_move_window(shyft_hip_region* h, size_t w0, int fill_mask) {
     if (!h) return fail(h, "shyft_hip_set_window: null handle");
     return guarded(h, [&] {
         if (h->T == 0) throw std::runtime_error("set_window: no time axis");
         if (w0 + h->TW > h->T) throw std::runtime_error("set_window: window beyond the time axis");
         h->w0 = w0;
-        hip_check(launch_fill(h->d_forcing.p, h->d_forcing.n, NAN, h->stream), "fill");
-        hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill");
-        if (h->d_state_series.p) hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill");
+        if (fill_mask & 1) hip_check(launch_fill(h->d_forcing.p, h->d_forcing.n, NAN, h->stream), "fill");
+        if (fill_mask & 2) hip_check(launch_fill(h->d_resp.p, h->d_resp.n, NAN, h->stream), "fill");
+        if ((fill_mask & 4) && h->d_state_series.p)
+            hip_check(launch_fill(h->d_state_series.p, h->d_state_series.n, NAN, h->stream), "fill");
         hip_check(hipStreamSynchronize(h->stream), "sync");
     });
 }
@@ -757,6 +760,7 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
         g.default_gradient = idw_param[4];
         g.src_xyz = h->d_src_xyz.p;
         g.src_values = h->d_src_vals.p;
+        g.dst_xyz = h->d_dst_xyz.p;
         g.slope = h->d_slope.p;
         g.idx = tab.idx.p;
         g.w = tab.w.p;

@@ -85,6 +85,10 @@ class HipRegion:
     def set_window(self, w0: int):
         self._chk(self._L.shyft_hip_set_window(self.h, int(w0)))
 
+    def move_window(self, w0: int, fill_mask: int = 0):
+        """set_window without (or with a subset of) the NaN fill; for callers that rewrite the whole window."""
+        self._chk(self._L.shyft_hip_move_window(self.h, int(w0), int(fill_mask)))
+
     def set_collection(self, collect: int, collect_state: bool = False):
         self._chk(self._L.shyft_hip_set_collection(self.h, int(collect), int(bool(collect_state))))
 
