@@ -7,6 +7,11 @@
 // the two variants to bound the effect of the elementary-function library.
 // The incomplete gamma (boost::math::gamma_p in the reference) always comes
 // from detmath::gamma_pq, evaluated with this build's exp/log.
+//
+// The reference writes every power as std::pow. The detmath build evaluates
+// the small integer powers by squaring (OPOW4, OPOW8) and the fractional powers
+// of moderate arguments and odeint's step-size controller as exp(y log x)
+// (OPOWR); the libm build keeps std::pow for all of them.
 #pragma once
 #include <cmath>
 
@@ -16,10 +21,16 @@
 #define OEXP(x) std::exp(x)
 #define OLOG(x) std::log(x)
 #define OPOW(x, y) std::pow(x, y)
+#define OPOW4(x) std::pow(x, 4)
+#define OPOW8(x) std::pow(x, 8)
+#define OPOWR(x, y) std::pow(x, y)
 #define OLGAMMA(x) std::lgamma(x)
 #else
 #define OEXP(x) detmath::exp(x)
 #define OLOG(x) detmath::log(x)
 #define OPOW(x, y) detmath::pow((double)(x), (double)(y))
+#define OPOW4(x) detmath::pow4((double)(x))
+#define OPOW8(x) detmath::pow8((double)(x))
+#define OPOWR(x, y) detmath::powr((double)(x), (double)(y))
 #define OLGAMMA(x) detmath::lgamma(x)
 #endif

@@ -45,8 +45,8 @@ struct calculator {
     // priestley_taylor.h:97-102
     double net_radiation(double temperature, double global_radiation, double rhumidity, double vapour_pressure) const {
         double k_temp = temperature + 273.15;
-        double e_atm = 1.24 * OPOW(10 * vapour_pressure / k_temp, 0.143) * (0.85 + 0.5 * rhumidity);
-        return bolz * OPOW(k_temp, 4) * (e_atm - 0.98) + global_radiation * (1.0 - land_albedo);
+        double e_atm = 1.24 * OPOWR(10 * vapour_pressure / k_temp, 0.143) * (0.85 + 0.5 * rhumidity);
+        return bolz * OPOW4(k_temp) * (e_atm - 0.98) + global_radiation * (1.0 - land_albedo);
     }
 };
 }  // namespace priestley_taylor
@@ -325,7 +325,7 @@ struct calculator {
 
         const double T_k = T + 273.15;
         const double turb = p.wind_scale * wind_speed + p.wind_const;
-        double vapour_pressure = 33.864 * (OPOW(7.38e-3 * T + 0.8072, 8) - 1.9e-5 * std::fabs(1.8 * T + 48.0) + 1.316e-3) * rel_hum;
+        double vapour_pressure = 33.864 * (OPOW8(7.38e-3 * T + 0.8072) - 1.9e-5 * std::fabs(1.8 * T + 48.0) + 1.316e-3) * rel_hum;
         if (T < 0.0) vapour_pressure *= 1.0 + 9.72e-3 * T + 4.2e-5 * T * T;
 
         if (snow > tol)
@@ -337,7 +337,7 @@ struct calculator {
         albedo = std::max(std::min(albedo, max_albedo), min_albedo);
 
         double effect = rad * (1.0 - albedo);
-        effect += 0.98 * sigma * OPOW(vapour_pressure / T_k, 6.87e-2) * OPOW(T_k, 4);
+        effect += 0.98 * sigma * OPOWR(vapour_pressure / T_k, 6.87e-2) * OPOW4(T_k);
         if (T > 0.0 && snow < tol) effect += rain * T * water_heat / dt_s;
         if (T <= 0.0 && rain < tol) effect += snow * T * ice_heat / dt_s;
 
@@ -351,7 +351,7 @@ struct calculator {
             effect += turb * (T + 1.7 * (vapour_pressure - 6.12)) - BB0;
         else
             effect += turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * OEXP(0.103 * T - 0.186)))
-                      - 0.98 * sigma * OPOW(sst + 273.15, 4);
+                      - 0.98 * sigma * OPOW4(sst + 273.15);
 
         double delta_sh = -surface_heat;
         surface_heat = p.surface_magnitude * ice_heat * sst * 0.5;
@@ -500,7 +500,7 @@ struct calculator {
             const double err = std::fabs(xerr) / (abs_err + rel_err * (1.0 * std::fabs(x) + 1.0 * dt * std::fabs(dxdt)));
             s.k3 = k3; s.k4 = k4; s.k5 = k5; s.k6 = k6;
             if (err > 1.0) {
-                s.dt = dt * std::max(0.9 * OPOW(err, -1.0 / 3.0), 1.0 / 5.0);
+                s.dt = dt * std::max(0.9 * OPOWR(err, -1.0 / 3.0), 1.0 / 5.0);
                 if (++attempts >= 500) throw std::runtime_error("kirchner: odeint max number of iterations exceeded (500)");
                 continue;
             }
@@ -508,7 +508,7 @@ struct calculator {
             double ndt = dt;
             if (err < 0.5) {
                 const double e2 = std::max(0.00032, err);  // pow(5.0,-5.0), correctly rounded
-                ndt = dt * (9.0 / 10.0 * OPOW(e2, -1.0 / 5.0));
+                ndt = dt * (9.0 / 10.0 * OPOWR(e2, -1.0 / 5.0));
             }
             s.dt = ndt;
             s.x_old = x; s.dxdt_old = dxdt;

@@ -71,6 +71,24 @@ def header_symbols(header: str | None = None) -> list[str]:
     return sorted(set(re.findall(r"\b(shyft_hip_[a-z_0-9]+)\s*\(", src)))
 
 
+def _preload_hip_runtime() -> None:
+    """Load the HIP runtime PyTorch ships (if PyTorch is installed) before libshyft_hip.so.
+
+    A process must hold ONE HIP runtime. libshyft_hip.so links libamdhip64 by soname; if it is loaded
+    first, /opt/rocm's copy is mapped and a later torch.cuda initialisation (torch carries its own copy)
+    finds no GPU. Mapping torch's copy first (RTLD_GLOBAL) makes both resolve to it. The torch package
+    itself is not imported."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+            return
+
+
 def lib() -> C.CDLL:
     global _LIB
     if _LIB is not None:
@@ -79,6 +97,7 @@ def lib() -> C.CDLL:
         if _LIB is None:
             if not os.path.exists(LIB_PATH):
                 raise RuntimeError(f"shyft_amd: HIP library not built ({LIB_PATH}); run __graft_entry__.build()")
+            _preload_hip_runtime()
             L = C.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 f = getattr(L, name)

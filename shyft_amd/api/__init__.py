@@ -13,6 +13,10 @@ from __future__ import annotations
 
 import numpy as np
 
+from .._native import lib as _lib
+
+_lib()  # one HIP runtime per process: map it (and libshyft_hip.so) before the extension module
+
 from ._api import (  # noqa: F401  (re-exported names)
     GeoPoint, LandTypeFractions, RoutingInfo, GeoCellData, TimeAxisFixedDeltaT, point_interpretation_policy,
     POINT_INSTANT_VALUE, POINT_AVERAGE_VALUE, IDWParameter, IDWTemperatureParameter, IDWPrecipitationParameter,

@@ -18,8 +18,8 @@ __device__ SHYFT_INL_PT double pt_pot_evap(double albedo, double alpha, double t
     const double delta = sat_pressure * ck2 * ck3 * ctt_inv * ctt_inv;
     const double vapour_pressure = sat_pressure * rhumidity;
     const double k_temp = temperature + 273.15;
-    const double e_atm = 1.24 * dpow(10 * vapour_pressure / k_temp, 0.143) * (0.85 + 0.5 * rhumidity);
-    const double net_rad = 0.0000000567 * dpow(k_temp, 4.0) * (e_atm - 0.98) + global_radiation * (1.0 - albedo);
+    const double e_atm = 1.24 * dpowr(10 * vapour_pressure / k_temp, 0.143) * (0.85 + 0.5 * rhumidity);
+    const double net_rad = 0.0000000567 * dpow4(k_temp) * (e_atm - 0.98) + global_radiation * (1.0 - albedo);
     const double epot = alpha * delta * net_rad / (delta + 0.066);
     if (epot < 0.0) return 0.0;
     return epot / (2500780 - 2361 * temperature);

@@ -195,7 +195,7 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
 
     const double T_k = T + 273.15;
     const double turb = P[PK_WIND_SCALE] * wind_speed + P[PK_WIND_CONST];
-    double vapour_pressure = 33.864 * (dpow(7.38e-3 * T + 0.8072, 8.0) - 1.9e-5 * fabs(1.8 * T + 48.0) + 1.316e-3) * rel_hum;
+    double vapour_pressure = 33.864 * (dpow8(7.38e-3 * T + 0.8072) - 1.9e-5 * fabs(1.8 * T + 48.0) + 1.316e-3) * rel_hum;
     if (T < 0.0) vapour_pressure *= 1.0 + 9.72e-3 * T + 4.2e-5 * T * T;
 
     if (snow > GS_TOL)
@@ -208,7 +208,7 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
 
     const double sigma = 5.670373e-8;
     double effect = rad * (1.0 - albedo);
-    effect += 0.98 * sigma * dpow(vapour_pressure / T_k, 6.87e-2) * dpow(T_k, 4.0);
+    effect += 0.98 * sigma * dpowr(vapour_pressure / T_k, 6.87e-2) * dpow4(T_k);
     if (T > 0.0 && snow < GS_TOL) effect += rain * T * 4180.0 / dt_s;
     if (T <= 0.0 && rain < GS_TOL) effect += snow * T * 2050.0 / dt_s;
 
@@ -221,7 +221,7 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
         effect += turb * (T + 1.7 * (vapour_pressure - 6.12)) - P[PK_BB0];
     else
         effect += turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * dexp(0.103 * T - 0.186))) -
-                  0.98 * sigma * dpow(sst + 273.15, 4.0);
+                  0.98 * sigma * dpow4(sst + 273.15);
 
     double delta_sh = -surface_heat;
     surface_heat = P[PK_SURFACE_MAG] * 2050.0 * sst * 0.5;
@@ -410,7 +410,7 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         const double xerr = dt * dc1 * dxdt + dt * dc3 * s3 + dt * dc4 * s4 + dt * dc5 * s5 + dt * dc6 * s6 + dt * dc7 * dxdt_o;
         const double err = fabs(xerr) / (abs_err + rel_err * (1.0 * fabs(x) + 1.0 * dt * fabs(dxdt)));
         if (err > 1.0) {
-            dt = dt * smax(0.9 * dpow(err, -1.0 / 3.0), 1.0 / 5.0);
+            dt = dt * smax(0.9 * dpowr(err, -1.0 / 3.0), 1.0 / 5.0);
             if (++attempts >= 500) { ok = false; break; }
             continue;
         }
@@ -419,7 +419,7 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         t = t + dt;
         if (err < 0.5) {
             const double e2 = smax(0.00032, err);  // dpow(5.0, -5.0)
-            dt = dt * (9.0 / 10.0 * dpow(e2, -1.0 / 5.0));
+            dt = dt * (9.0 / 10.0 * dpowr(e2, -1.0 / 5.0));
         }
         x_old = x; dxdt_old = dxdt;
         x = xo; dxdt = dxdt_o;

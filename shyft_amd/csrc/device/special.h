@@ -47,6 +47,10 @@ __device__ SHYFT_DM_INLINE double dexp(double x) { return detmath::exp(x); }
 __device__ SHYFT_DM_INLINE double dlog(double x) { return detmath::log(x); }
 __device__ SHYFT_DM_INLINE_POW double dpow(double x, double y) { return detmath::pow(x, y); }
 __device__ __noinline__ double dlgamma(double x) { return detmath::lgamma(x); }
+// structured powers (detmath::pow4 / pow8 / powr, the oracle's OPOW4 / OPOW8 / OPOWR)
+__device__ __forceinline__ double dpow4(double x) { return detmath::pow4(x); }
+__device__ __forceinline__ double dpow8(double x) { return detmath::pow8(x); }
+__device__ inline double dpowr(double x, double y) { return dexp(y * dlog(x)); }
 
 // boost::math::gamma_p stand-in: detmath::gamma_pq (P(a,x), P(a+1,x) and the
 // prefix x^a e^-x / Gamma(a) from ONE series / continued-fraction evaluation),

@@ -12,6 +12,7 @@ struct ptgsk_kargs {
     int win0;         // absolute step of window row 0
     int win_len;      // window rows (forcing/response stride)
     int collect;      // collect_mode
+    int uniform_params;  // 1: every cell uses parameter set 0 (n_sets == 1)
     double dt_s;      // to_seconds(dt)
     double dt_us;     // dt in microseconds (as double)
     double t1_hours;  // kirchner integration end: to_seconds(dt)/3600

@@ -33,7 +33,10 @@ constexpr int BLOCK = SHYFT_BLOCK;
 #define SHYFT_LB_WAVES 4
 #endif
 
-template <bool COMPACT>
+// UNIFORM: every cell of the launch uses parameter set 0 (the region parameter, no catchment overrides):
+// the parameter row is then wave-uniform and lives in SGPRs (scalar loads), which frees the VGPRs the
+// per-lane copies would take in the register-bound time loop.
+template <bool COMPACT, bool UNIFORM>
 __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
@@ -41,7 +44,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     if (!COMPACT && !valid) return;
     const int lc = valid ? cell : 0;  // out-of-range lanes of a COMPACT block read cell 0 and store nothing
     const size_t N = (size_t)a.n_cells;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
+    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
 
     // per-cell constants (pt_gs_k.h:347-357)
     const double* __restrict__ cc = a.cellc;
@@ -220,8 +223,9 @@ hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
     if (SHYFT_COMPACT_DEFAULT)
-        hipLaunchKernelGGL(ptgsk_run_kernel<true>, dim3(grid), dim3(BLOCK), 0, stream, a);
+        if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else
-        hipLaunchKernelGGL(ptgsk_run_kernel<false>, dim3(grid), dim3(BLOCK), 0, stream, a);
+        hipLaunchKernelGGL((ptgsk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

@@ -842,6 +842,7 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     a.win0 = int(h->w0);
     a.win_len = int(h->TW);
     a.collect = h->collect;
+    a.uniform_params = h->n_sets == 1 ? 1 : 0;
     a.dt_s = double(h->dt) / 1e6;
     a.dt_us = double(h->dt);
     a.t1_hours = a.dt_s / 3600.0;  // to_seconds(T1-T0)/to_seconds(deltahours(1))
