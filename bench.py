@@ -122,8 +122,12 @@ def dist_setup(n_gpus):
     if world > 1:
         import torch
         import torch.distributed as dist
+        # one rank per GPU (RCCL over xGMI). SHYFT_DIST_BACKEND=gloo + more ranks than GPUs is only for
+        # rehearsing the multi-rank path on a one-GPU box; the device index wraps in that case.
+        n_dev = torch.cuda.device_count()
+        local = local % n_dev if n_dev else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("SHYFT_DIST_BACKEND", "nccl"))
         pg = dist
     return world, rank, local, pg
 
