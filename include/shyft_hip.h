@@ -194,6 +194,25 @@ int shyft_hip_route(int device, size_t n_groups, size_t T, const double* group_s
                     const double* river_uhg, const int32_t* river_len, const int32_t* river_downstream, size_t max_len,
                     double* local, double* upstream, double* output, int dst_on_device);
 
+/* ---- parameter ensembles for calibration (core/model_calibration.h:830-899) ----
+ * The reference optimizer evaluates one parameter vector per region run: set parameters, revert to the
+ * initial state, run_cells over the calculated catchments, sum catchment discharge, score against the
+ * targets. shyft_hip_ensemble_run evaluates n_members parameter vectors in ONE launch: its lanes are
+ * (calculated cell, member) pairs, member-fastest, each starting from the region's current state and
+ * reading the region's forcing in place (shared, not copied). The region's own state and responses are
+ * not modified. params[n_members][n_per_set] in the reference get/set order (as shyft_hip_set_parameters).
+ * collect: SHYFT_HIP_COLLECT_DISCHARGE or SHYFT_HIP_COLLECT_DISCHARGE_SNOW (adds snow sca / swe). */
+int shyft_hip_ensemble_run(shyft_hip_region* h, const double* params, size_t n_members, size_t n_per_set,
+                           int start_step, int n_steps, int collect);
+/* Sums of response `series` of the last ensemble run per member and catchment, steps [step0, step0+n)
+ * inside its run range: dst[n_members][n_catchments][n], catchments in shyft_hip_catchment_ids order
+ * (uncalculated catchments sum to 0). area_weighted != 0: sum of value x cell area (the area-weighted
+ * snow sums of model_calibration.h:765-776). */
+int shyft_hip_ensemble_sums(const shyft_hip_region* h, int series, int area_weighted, size_t step0, size_t n,
+                            double* dst, int dst_on_device);
+/* Milliseconds of the last ensemble launch (HIP events on its stream). */
+double shyft_hip_ensemble_last_ms(const shyft_hip_region* h);
+
 /* Diagnostic: evaluate one device elementary function (0 exp, 1 log, 2 pow(x, y), 3 lgamma,
  * 4 gamma_p(x, y)) on n host inputs on the current device; out[n] host. Used by the parity
  * tests to show device math == host math bit for bit. */

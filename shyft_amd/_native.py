@@ -59,6 +59,9 @@ SIGNATURES = {
     "shyft_hip_route": (C.c_int, [C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_int]),
+    "shyft_hip_ensemble_run": (C.c_int, [_h, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int]),
+    "shyft_hip_ensemble_sums": (C.c_int, [_h, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
+    "shyft_hip_ensemble_last_ms": (C.c_double, [_h]),
     "shyft_hip_math_selftest": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
 }
 

@@ -20,7 +20,8 @@ _lib()  # one HIP runtime per process: map it (and libshyft_hip.so) before the e
 from ._api import (  # noqa: F401  (re-exported names)
     GeoPoint, LandTypeFractions, RoutingInfo, GeoCellData, TimeAxisFixedDeltaT, point_interpretation_policy,
     POINT_INSTANT_VALUE, POINT_AVERAGE_VALUE, IDWParameter, IDWTemperatureParameter, IDWPrecipitationParameter,
-    InterpolationParameter, UHGParameter, River, RiverNetwork, make_uhg_from_gamma, average_values,
+    InterpolationParameter, UHGParameter, River, RiverNetwork, make_uhg_from_gamma, average_values, FlowAdjustResult,
+    find_min_single_variable,
 )
 from . import _api
 
@@ -543,6 +544,14 @@ class _ModelMixin:
     def run_cells(self, use_ncore=0, start_step=0, n_steps=0):
         self._push_parameters()
         super().run_cells(use_ncore, start_step, n_steps)
+
+    def adjust_state_to_target_flow(self, wanted_flow_m3s, cids, start_step=0, scale_range=3.0, scale_eps=1e-3,
+                                    max_iter=300, n_steps=1):
+        """Tune the discharge state of `cids` so the average flow over [start_step, start_step+n_steps) is
+        wanted_flow_m3s (region_model.h:626-637); returns FlowAdjustResult(q_0, q_r, diagnostics)."""
+        self._push_parameters()
+        return super().adjust_state_to_target_flow(float(wanted_flow_m3s), list(cids), int(start_step),
+                                                   float(scale_range), float(scale_eps), int(max_iter), int(n_steps))
 
     # states
     def set_states(self, states):

@@ -11,6 +11,7 @@
 // internally it is int64 microseconds.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/functional.h>
 #include <pybind11/stl.h>
 
 #include <cmath>
@@ -67,6 +68,9 @@ void bind_model(py::module_& m, const char* name) {
         .def("_set_states", &M::set_states)
         .def("revert_to_initial_state", &M::revert_to_initial_state)
         .def("adjust_q", &M::adjust_q, py::arg("q_scale"), py::arg("cids"))
+        .def("adjust_state_to_target_flow", &M::adjust_state_to_target_flow, py::arg("wanted_flow_m3s"),
+             py::arg("cids"), py::arg("start_step") = 0, py::arg("scale_range") = 3.0, py::arg("scale_eps") = 1e-3,
+             py::arg("max_iter") = 300, py::arg("n_steps") = 1)
         .def("set_state_collection", &M::set_state_collection, py::arg("catchment_id"), py::arg("on_or_off"))
         .def("set_snow_sca_swe_collection", &M::set_snow_sca_swe_collection, py::arg("catchment_id"), py::arg("on_or_off"))
         .def("_cell_collects_state", &M::cell_collects_state)
@@ -265,6 +269,21 @@ PYBIND11_MODULE(_api, m) {
                       [](river& r, const routing_info& ri) { r.downstream_id = ri.id; r.downstream_distance = ri.distance; })
         .def_readwrite("parameter", &river::parameter)
         .def("uhg", [](const river& r, double dt) { return r.uhg(to_us(dt)); });
+    py::class_<q_adjust_result>(m, "FlowAdjustResult")
+        .def(py::init<>())
+        .def_readwrite("q_0", &q_adjust_result::q_0)
+        .def_readwrite("q_r", &q_adjust_result::q_r)
+        .def_readwrite("diagnostics", &q_adjust_result::diagnostics);
+    // the state tuner's 1-D minimiser, exposed for host-side tests (no device work)
+    m.def(
+        "find_min_single_variable",
+        [](const std::function<double(double)>& f, double x, double begin, double end, double eps, long max_iter,
+           double radius) {
+            const double fx = find_min_single_variable(f, x, begin, end, eps, max_iter, radius);
+            return std::make_pair(x, fx);
+        },
+        py::arg("f"), py::arg("starting_point"), py::arg("begin"), py::arg("end"), py::arg("eps") = 1e-3,
+        py::arg("max_iter") = 100, py::arg("initial_search_radius") = 1.0);
     py::class_<river_network>(m, "RiverNetwork")
         .def(py::init<>())
         .def("add", [](river_network& n, const river& r) -> river_network& { return n.add(r); }, py::return_value_policy::reference_internal)

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../../include/shyft_hip.h"
+#include "optimize.hpp"
 #include "routing.hpp"
 #include "time_series.hpp"
 
@@ -174,6 +175,13 @@ struct pt_ss_k_stack {
 };
 
 // ---- region_model ------------------------------------------------------------------------------------------------
+// result of adjust_state_to_target_flow (core/model_state_tuning.h:12-17)
+struct q_adjust_result {
+    double q_0{0.0};          // m3/s with the state before adjustment
+    double q_r{0.0};          // m3/s with the adjusted state
+    std::string diagnostics;  // empty if ok
+};
+
 template <class Stack>
 class region_model {
   public:
@@ -411,6 +419,55 @@ class region_model {
             if (cids.empty() || std::find(cids.begin(), cids.end(), geo_[i].catchment_id()) != cids.end())
                 s[i][Stack::state_q] *= q_scale;
         put_states(s);
+    }
+
+    // ---- state tuning to a wanted flow (region_model.h:626-637, core/model_state_tuning.h:35-120)
+    // Scales the discharge state of the cells in `cids` (adjust_q) so that the average summed discharge over
+    // steps [start_step, start_step+n_steps) equals wanted_flow_m3s; the scale is searched in
+    // [s/scale_range, s*scale_range] around s = wanted/q_0 with find_min_single_variable. Each evaluation
+    // restores the snapshot state, scales it, runs the filtered cells for n_steps on the device and sums
+    // discharge there. On return the current state is the tuned one; the calculation filter is restored.
+    q_adjust_result adjust_state_to_target_flow(double wanted_flow_m3s, const std::vector<int64_t>& cids,
+                                                size_t start_step = 0, double scale_range = 3.0, double scale_eps = 1e-3,
+                                                size_t max_iter = 300, size_t n_steps = 1) {
+        std::vector<int64_t> old_filter;
+        for (size_t c = 0; c < catchment_filter_.size(); ++c)
+            if (catchment_filter_[c]) old_filter.push_back(cix_to_cid_[c]);
+        q_adjust_result r;
+        try {
+            set_catchment_calculation_filter(cids);
+            const std::vector<state_t> s0 = current_state();
+            auto discharge = [&](double q_scale) {
+                put_states(s0);
+                adjust_q(q_scale, cids);
+                run_cells(0, int(start_step), int(n_steps));
+                double q_sum = 0.0;
+                for (size_t i = start_step; i < start_step + n_steps; ++i)
+                    q_sum += stat_value(0, cids, SHYFT_HIP_SCOPE_CATCHMENT, false, i);
+                return q_sum / double(n_steps);
+            };
+            r.q_0 = discharge(1.0);
+            double scale = wanted_flow_m3s / r.q_0;
+            try {
+                if (!std::isfinite(r.q_0)) throw std::runtime_error("the initial simulated discharge is nan");
+                find_min_single_variable(
+                    [&](double x) {
+                        const double d = discharge(x) - wanted_flow_m3s;
+                        return d * d;
+                    },
+                    scale, scale / scale_range, scale * scale_range, scale * scale_eps, long(max_iter));
+            } catch (const std::exception& e) {
+                r.diagnostics = std::string("failed to find solution within ") + std::to_string(max_iter) +
+                                std::string(", exception was:") + e.what();
+            }
+            r.q_r = discharge(scale);
+            put_states(s0);
+            adjust_q(scale, cids);
+        } catch (const std::exception& e) {
+            r.diagnostics = std::string("Failed to tune_flow") + e.what();
+        }
+        set_catchment_calculation_filter(old_filter);
+        return r;
     }
 
     // ---- collection (region_model.h:806-818)

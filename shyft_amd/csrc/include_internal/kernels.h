@@ -22,7 +22,9 @@ struct ptgsk_kargs {
     const int32_t* set_ix;         // [N]
     const double* cellc;           // [PTGSK_NC][N]
     double* state;                 // [PTGSK_NS][N]
-    const double* forcing;         // [N_FORCING][win_len][N]
+    const double* forcing;         // [N_FORCING][win_len][f_cols]
+    const int32_t* fcol;           // [N] forcing column of each lane (parameter ensembles), null = lane
+    int f_cols;                    // forcing columns (== n_cells unless fcol is set)
     double* resp;                  // [n_series][win_len][N]
     double* state_series;          // [PTGSK_NS][win_len+1][N] or null
     const uint8_t* active;         // [N] catchment filter or null
@@ -39,7 +41,9 @@ struct hbv_kargs {
     const int32_t* set_ix;   // [N]
     const double* cellc;     // [HBV_NC][N]
     double* state;           // [HBV_NS][N]
-    const double* forcing;   // [N_FORCING][win_len][N]
+    const double* forcing;   // [N_FORCING][win_len][f_cols]
+    const int32_t* fcol;     // [N] forcing column of each lane, null = lane
+    int f_cols;              // forcing columns
     double* resp;            // [n_series][win_len][N]
     double* state_series;    // [HBV_NS][win_len+1][N] or null
     const uint8_t* active;   // [N] or null
@@ -57,7 +61,9 @@ struct ptssk_kargs {
     const int32_t* set_ix;   // [N]
     const double* cellc;     // [PTGSK_NC][N]
     double* state;           // [PTSSK_NS][N]
-    const double* forcing;   // [N_FORCING][win_len][N]
+    const double* forcing;   // [N_FORCING][win_len][f_cols]
+    const int32_t* fcol;     // [N] forcing column of each lane, null = lane
+    int f_cols;              // forcing columns
     double* resp;            // [n_series][win_len][N]
     double* state_series;    // [PTSSK_NSC][win_len+1][N] or null
     const uint8_t* active;   // [N] or null
@@ -97,8 +103,14 @@ hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_step
                              const double* w, double* out, hipStream_t stream);
 
 // per-catchment sums: out[c][t] = sum over cells of segment c (seg_cells[seg_off[c]..seg_off[c+1]))
+// (w != null: sum of series * w[cell], the area-weighted sums of model_calibration.h:765-776)
 hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
-                               const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream);
+                               const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream,
+                               const double* w = nullptr);
+
+// dst[r][l] = src[r][idx[l]] for r < n_rows, l < n_lanes (parameter-ensemble lane replication)
+hipError_t launch_gather_columns(double* dst, const double* src, size_t n_rows, size_t src_cols, const int32_t* idx,
+                                 size_t n_lanes, hipStream_t stream);
 
 // flag = 1 if any of rows x cells (restricted to active cells when active != null) is NaN
 hipError_t launch_nan_scan(const double* f, size_t n_rows, size_t n_cells, const uint8_t* active, int32_t* flag,

@@ -36,7 +36,8 @@ constexpr int BLOCK = SHYFT_BLOCK;
 // UNIFORM: every cell of the launch uses parameter set 0 (the region parameter, no catchment overrides):
 // the parameter row is then wave-uniform and lives in SGPRs (scalar loads), which frees the VGPRs the
 // per-lane copies would take in the register-bound time loop.
-template <bool COMPACT, bool UNIFORM>
+// ENS: a parameter-ensemble launch (lanes = cells x members): forcing is read from the shared column fcol[lane].
+template <bool COMPACT, bool UNIFORM, bool ENS = false>
 __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
@@ -44,6 +45,8 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     if (!COMPACT && !valid) return;
     const int lc = valid ? cell : 0;  // out-of-range lanes of a COMPACT block read cell 0 and store nothing
     const size_t N = (size_t)a.n_cells;
+    const size_t NF = ENS ? (size_t)a.f_cols : N;
+    const size_t fcl = ENS ? (size_t)a.fcol[lc] : (size_t)lc;
     const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
 
     // per-cell constants (pt_gs_k.h:347-357)
@@ -84,11 +87,11 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     int32_t err = 0;
 
     const size_t TW = (size_t)a.win_len;
-    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * N;
-    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * N;
-    const double* __restrict__ f_ws = a.forcing + (size_t)FV_WIND_SPEED * TW * N;
-    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * N;
-    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * N;
+    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * NF;
+    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * NF;
+    const double* __restrict__ f_ws = a.forcing + (size_t)FV_WIND_SPEED * TW * NF;
+    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * NF;
+    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * NF;
     double* __restrict__ R = a.resp;
     const size_t RS = TW * N;  // stride between response series
     double* __restrict__ SS = a.state_series;
@@ -122,13 +125,14 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + lc;
+        const size_t ff = ENS ? wi * NF + fcl : fo;
         double temp = 0, rad = 0, rel_hum = 0, prec = 0, wind_speed = 0;
         if (valid) {
-            temp = f_temp[fo];
-            rad = f_rad[fo];
-            rel_hum = f_rh[fo];
-            prec = f_prec[fo] * p_corr;
-            wind_speed = f_ws[fo];
+            temp = f_temp[ff];
+            rad = f_rad[ff];
+            rel_hum = f_rh[ff];
+            prec = f_prec[ff] * p_corr;
+            wind_speed = f_ws[ff];
             if (SS) collect_state(wi);
         }
         const bool start_melt = a.doy[i] == wed;
@@ -222,7 +226,9 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
 hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (SHYFT_COMPACT_DEFAULT)
+    if (a.fcol)
+        hipLaunchKernelGGL((ptgsk_run_kernel<true, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (SHYFT_COMPACT_DEFAULT)
         if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
         else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else

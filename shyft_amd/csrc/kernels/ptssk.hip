@@ -28,6 +28,9 @@ __global__ __launch_bounds__(BLOCK) void ptssk_run_kernel(const ptssk_kargs a) {
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;
     const size_t N = (size_t)a.n_cells;
+    // forcing column: the lane itself, or the shared cell of a parameter-ensemble lane
+    const size_t NF = a.fcol ? (size_t)a.f_cols : N;
+    const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
     const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * PTSSK_NP;
 
     ss_par sp;
@@ -68,10 +71,10 @@ __global__ __launch_bounds__(BLOCK) void ptssk_run_kernel(const ptssk_kargs a) {
     int32_t err = 0;
 
     const size_t TW = (size_t)a.win_len;
-    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * N;
-    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * N;
-    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * N;
-    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * N;
+    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * NF;
+    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * NF;
+    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * NF;
+    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * NF;
     double* __restrict__ R = a.resp;
     const size_t RS = TW * N;
     double* __restrict__ SS = a.state_series;
@@ -96,10 +99,11 @@ __global__ __launch_bounds__(BLOCK) void ptssk_run_kernel(const ptssk_kargs a) {
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
-        const double temp = f_temp[fo];
-        const double rad = f_rad[fo];
-        const double rel_hum = f_rh[fo];
-        const double prec = f_prec[fo] * p_corr;
+        const size_t ff = wi * NF + fcl;
+        const double temp = f_temp[ff];
+        const double rad = f_rad[ff];
+        const double rel_hum = f_rh[ff];
+        const double prec = f_prec[ff] * p_corr;
         if (SS) collect_state(wi);
         double snow_outflow, snow_sca, snow_swe;
         ss_step(sp, a.step_in_days, a.dt_hours, temp, prec, s, snow_outflow, snow_sca, snow_swe, err);

@@ -8,6 +8,7 @@
 // then a fixed-shape wavefront shuffle tree + LDS combine, so results are
 // bitwise reproducible run to run (no float atomics).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 
 #include "../include_internal/kernels.h"
@@ -53,13 +54,18 @@ __global__ __launch_bounds__(RB) void select_sum_kernel(const double* __restrict
 
 __global__ __launch_bounds__(RB) void segment_sum_kernel(const double* __restrict__ series, size_t n_cells, size_t n_steps,
                                                          const int32_t* __restrict__ seg_cells,
-                                                         const int32_t* __restrict__ seg_off, double* __restrict__ out) {
+                                                         const int32_t* __restrict__ seg_off, double* __restrict__ out,
+                                                         const double* __restrict__ w) {
     const size_t t = blockIdx.x;
     const size_t c = blockIdx.y;
     const double* __restrict__ row = series + t * n_cells;
     const int32_t b = seg_off[c], e = seg_off[c + 1];
     double acc = 0.0;
-    for (int32_t k = b + (int32_t)threadIdx.x; k < e; k += RB) acc += row[seg_cells[k]];
+    if (w) {
+        for (int32_t k = b + (int32_t)threadIdx.x; k < e; k += RB) acc += row[seg_cells[k]] * w[seg_cells[k]];
+    } else {
+        for (int32_t k = b + (int32_t)threadIdx.x; k < e; k += RB) acc += row[seg_cells[k]];
+    }
     const double r = block_sum(acc);
     if (threadIdx.x == 0) out[c * n_steps + t] = r;
 }
@@ -81,7 +87,26 @@ __global__ void fill_kernel(double* __restrict__ p, size_t n, double v) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// dst[r][l] = src[r][idx[l]]: replicate cell columns into parameter-ensemble lanes
+__global__ void gather_columns_kernel(double* __restrict__ dst, const double* __restrict__ src, size_t n_rows,
+                                      size_t src_cols, const int32_t* __restrict__ idx, size_t n_lanes) {
+    const size_t total = n_rows * n_lanes;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / n_lanes, l = i - r * n_lanes;
+        dst[i] = src[r * src_cols + (size_t)idx[l]];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_gather_columns(double* dst, const double* src, size_t n_rows, size_t src_cols, const int32_t* idx,
+                                 size_t n_lanes, hipStream_t stream) {
+    const size_t total = n_rows * n_lanes;
+    if (total == 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(gather_columns_kernel, dim3(grid), dim3(256), 0, stream, dst, src, n_rows, src_cols, idx, n_lanes);
+    return hipGetLastError();
+}
 
 hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_steps, const int32_t* cells, size_t n_sel,
                              const double* w, double* out, hipStream_t stream) {
@@ -92,10 +117,10 @@ hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_step
 }
 
 hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
-                               const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream) {
+                               const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream, const double* w) {
     if (n_steps == 0 || n_seg == 0) return hipSuccess;
     hipLaunchKernelGGL(segment_sum_kernel, dim3((unsigned)n_steps, (unsigned)n_seg), dim3(RB), 0, stream, series, n_cells,
-                       n_steps, seg_cells, seg_off, out);
+                       n_steps, seg_cells, seg_off, out, w);
     return hipGetLastError();
 }
 

@@ -136,6 +136,13 @@ struct shyft_hip_region {
     dbuf<int32_t> d_rseg_cells, d_rseg_off;
     size_t n_route_groups = 0;
 
+    // parameter ensemble (calibration): a lane region of calculated cells x members that reads this
+    // region's forcing through d_fcol (see shyft_hip_ensemble_run)
+    shyft_hip_region* ens = nullptr;
+    const shyft_hip_region* forcing_src = nullptr;  // set on an ensemble lane region: whose forcing it reads
+    dbuf<int32_t> d_fcol;                            // [lanes] forcing column (cell of the parent region)
+    size_t ens_members = 0, ens_cells = 0, ens_groups = 0, ens_b = 0, ens_e = 0;
+
     bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
     bool ptssk() const { return stack == SHYFT_HIP_PT_SS_K; }
     size_t n_series() const {
@@ -436,6 +443,7 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
 
 void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (!h) return;
+    if (h->ens) shyft_hip_region_destroy(h->ens);
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -800,7 +808,9 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.set_ix = h->d_set_ix.p;
         a.cellc = h->d_cellc.p;
         a.state = h->d_state.p;
-        a.forcing = h->d_forcing.p;
+        a.forcing = h->forcing_src ? h->forcing_src->d_forcing.p : h->d_forcing.p;
+        a.fcol = h->forcing_src ? h->d_fcol.p : nullptr;
+        a.f_cols = int(h->forcing_src ? h->forcing_src->n : h->n);
         a.resp = h->d_resp.p;
         a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
         a.active = h->active.empty() ? nullptr : h->d_active.p;
@@ -825,7 +835,9 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.set_ix = h->d_set_ix.p;
         a.cellc = h->d_cellc.p;
         a.state = h->d_state.p;
-        a.forcing = h->d_forcing.p;
+        a.forcing = h->forcing_src ? h->forcing_src->d_forcing.p : h->d_forcing.p;
+        a.fcol = h->forcing_src ? h->d_fcol.p : nullptr;
+        a.f_cols = int(h->forcing_src ? h->forcing_src->n : h->n);
         a.resp = h->d_resp.p;
         a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
         a.active = h->active.empty() ? nullptr : h->d_active.p;
@@ -852,7 +864,9 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     a.set_ix = h->d_set_ix.p;
     a.cellc = h->d_cellc.p;
     a.state = h->d_state.p;
-    a.forcing = h->d_forcing.p;
+    a.forcing = h->forcing_src ? h->forcing_src->d_forcing.p : h->d_forcing.p;
+    a.fcol = h->forcing_src ? h->d_fcol.p : nullptr;
+    a.f_cols = int(h->forcing_src ? h->forcing_src->n : h->n);
     a.resp = h->d_resp.p;
     a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
     a.active = h->active.empty() ? nullptr : h->d_active.p;
@@ -1239,5 +1253,124 @@ int shyft_hip_route(int device, size_t n_groups, size_t T, const double* group_s
     }
     return 0;
 }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- parameter ensembles (core/model_calibration.h:830-899)
+extern "C" {
+
+int shyft_hip_ensemble_run(shyft_hip_region* h, const double* params, size_t n_members, size_t n_per_set,
+                           int start_step, int n_steps, int collect) {
+    if (!h || !params) return fail(h, "shyft_hip_ensemble_run: null argument");
+    return guarded(h, [&] {
+        if (n_members == 0) throw std::runtime_error("ensemble_run: n_members must be > 0");
+        if (collect != COLLECT_DISCHARGE && collect != COLLECT_DISCHARGE_SNOW)
+            throw std::runtime_error("ensemble_run: collect must be discharge or discharge+snow");
+        if (!h->has_geo) throw std::runtime_error("region: geo_cell_data not set");
+        if (!h->has_state) throw std::runtime_error("region_model::run: no state set");
+        if (!(h->T > 0)) throw std::runtime_error("region_model::run with invalid time_axis invoked");
+        if (start_step < 0 || n_steps < 0 || size_t(start_step) + size_t(n_steps) > h->T)
+            throw std::runtime_error("ensemble_run: steps outside the time axis");
+        const size_t b = n_steps > 0 ? size_t(start_step) : 0;
+        const size_t e = n_steps > 0 ? size_t(start_step + n_steps) : h->T;
+        check_window(h, b, e - b, "ensemble_run");
+        // calculated cells (catchment filter), cell order
+        std::vector<int32_t> cells;
+        for (size_t i = 0; i < h->n; ++i)
+            if (h->active.empty() || h->active[i]) cells.push_back(int32_t(i));
+        if (cells.empty()) throw std::runtime_error("ensemble_run: no calculated cells");
+        const size_t P = n_members, K = cells.size(), L = K * P;
+        if (L > size_t(INT32_MAX)) throw std::runtime_error("ensemble_run: cells x members exceeds 2^31 lanes");
+        hip_check(hipStreamSynchronize(h->stream), "sync");  // forcing/state writes of the region are complete
+
+        if (h->ens && (h->ens->n != L || h->ens->stack != h->stack)) {
+            shyft_hip_region_destroy(h->ens);
+            h->ens = nullptr;
+        }
+        if (!h->ens) {
+            shyft_hip_region* c = nullptr;
+            if (shyft_hip_region_create(h->stack, L, h->device, &c)) throw std::runtime_error(g_last_error);
+            h->ens = c;
+        }
+        shyft_hip_region* x = h->ens;
+        x->forcing_src = h;
+        x->geo.resize(L * 11);
+        std::vector<int32_t> fcol(L), lane_set(L);
+        for (size_t k = 0; k < K; ++k)
+            for (size_t m = 0; m < P; ++m) {
+                const size_t l = k * P + m;
+                fcol[l] = cells[k];
+                std::copy(h->geo.begin() + size_t(cells[k]) * 11, h->geo.begin() + size_t(cells[k]) * 11 + 11,
+                          x->geo.begin() + l * 11);
+                lane_set[l] = int32_t(m);
+            }
+        if (shyft_hip_set_parameters(x, params, P, n_per_set, lane_set.data())) throw std::runtime_error(x->err);
+        x->active.clear();
+        x->t0 = h->t0; x->dt = h->dt; x->T = h->T; x->w0 = h->w0; x->TW = h->TW;
+        x->collect = collect;
+        x->collect_state = 0;
+        x->has_geo = x->has_params = x->has_state = true;
+        x->derived_dirty = true;
+        update_derived(x);  // per-member parameter rows and per-lane constants
+        x->d_fcol.alloc(L);
+        hip_check(hipMemcpy(x->d_fcol.p, fcol.data(), L * sizeof(int32_t), hipMemcpyHostToDevice), "upload fcol");
+        clone_buf(x->d_doy, h->d_doy);
+        clone_buf(x->d_trel, h->d_trel);
+        // every member starts from the region's current state
+        hip_check(launch_gather_columns(x->d_state.p, h->d_state.p, h->n_state_fields(), h->n, x->d_fcol.p, L, x->stream),
+                  "gather state");
+        x->d_resp.alloc(x->n_series() * x->TW * L);
+        x->d_state_series.release();
+        // (member, catchment) segments, lanes in cell order: group m*C + cix
+        const size_t C = h->cix_to_cid.size();
+        std::vector<int32_t> off(P * C + 1, 0), seg(L);
+        for (size_t k = 0; k < K; ++k)
+            for (size_t m = 0; m < P; ++m) off[m * C + h->cix[size_t(cells[k])] + 1]++;
+        for (size_t g = 0; g < P * C; ++g) off[g + 1] += off[g];
+        std::vector<int32_t> pos(off.begin(), off.end() - 1);
+        for (size_t k = 0; k < K; ++k)
+            for (size_t m = 0; m < P; ++m) seg[size_t(pos[m * C + h->cix[size_t(cells[k])]]++)] = int32_t(k * P + m);
+        x->d_seg_off.alloc(off.size());
+        x->d_seg_cells.alloc(L);
+        hip_check(hipMemcpy(x->d_seg_off.p, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
+        hip_check(hipMemcpy(x->d_seg_cells.p, seg.data(), L * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
+        x->ens_groups = P * C;
+        h->ens_members = P;
+        h->ens_cells = K;
+        h->ens_b = b;
+        h->ens_e = e;
+        launch_run(x, int(b), int(e - b));
+        finish_run(x);
+    });
+}
+
+int shyft_hip_ensemble_sums(const shyft_hip_region* hc, int series, int area_weighted, size_t step0, size_t n,
+                            double* dst, int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_ensemble_sums: null argument");
+    return guarded(h, [&] {
+        shyft_hip_region* x = h->ens;
+        if (!x || h->ens_members == 0) throw std::runtime_error("ensemble_sums: no ensemble run");
+        if (series < 0 || size_t(series) >= x->n_series())
+            throw std::runtime_error("ensemble_sums: series not collected by the ensemble run");
+        if (step0 < h->ens_b || step0 + n > h->ens_e)
+            throw std::runtime_error("ensemble_sums: steps outside the last ensemble run");
+        const size_t L = x->n, G = x->ens_groups;
+        const double* src = x->d_resp.p + (size_t(series) * x->TW + (step0 - x->w0)) * L;
+        const double* w = nullptr;
+        if (area_weighted) w = x->d_cellc.p + size_t(x->hbv() ? HC_AREA : PC_AREA) * L;
+        double* out = dst;
+        if (!dst_on_device) {
+            x->d_tmp.alloc(std::max(x->d_tmp.n, G * n));
+            out = x->d_tmp.p;
+        }
+        hip_check(launch_segment_sums(src, L, n, x->d_seg_cells.p, x->d_seg_off.p, G, out, x->stream, w),
+                  "ensemble sums");
+        if (!dst_on_device) copy_rows(x->stream, dst, out, G * n * sizeof(double), 0, 1);
+        else hip_check(hipStreamSynchronize(x->stream), "sync");
+    });
+}
+
+double shyft_hip_ensemble_last_ms(const shyft_hip_region* h) { return h && h->ens ? h->ens->last_ms : 0.0; }
 
 }  // extern "C"

@@ -192,6 +192,24 @@ class HipRegion:
     def routing_group_sums_device(self, step0: int, n: int, dev_ptr: int):
         self._chk(self._L.shyft_hip_routing_group_sums(self.h, step0, n, C.c_void_p(dev_ptr), 1))
 
+    # parameter ensembles (model_calibration.h:830-899): n_members parameter vectors in one launch
+    def ensemble_run(self, params: np.ndarray, start_step: int = 0, n_steps: int = 0,
+                     collect: int = COLLECT_DISCHARGE):
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        assert p.ndim == 2
+        self._chk(self._L.shyft_hip_ensemble_run(self.h, _ptr(p), p.shape[0], p.shape[1], start_step, n_steps,
+                                                 collect))
+        self.ens_members = p.shape[0]
+
+    def ensemble_sums(self, series: int, step0: int, n: int, area_weighted: bool = False) -> np.ndarray:
+        """[n_members][n_catchments][n] sums of `series` over each member's calculated cells per catchment."""
+        out = np.empty((self.ens_members, self.number_of_catchments(), n), dtype=np.float64)
+        self._chk(self._L.shyft_hip_ensemble_sums(self.h, series, int(area_weighted), step0, n, _ptr(out), 0))
+        return out
+
+    def ensemble_last_ms(self) -> float:
+        return float(self._L.shyft_hip_ensemble_last_ms(self.h))
+
 
 def route(group_sums, group_uhgs, group_river, river_uhgs, river_downstream, device: int = -1, sums_dev_ptr=None,
           T: int | None = None):

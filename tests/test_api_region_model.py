@@ -184,6 +184,30 @@ def test_model_initialize_and_run():
     assert model.cells[0].state.kirchner.q == pytest.approx(q_0 * 2.0)
     model.revert_to_initial_state()
     model.run_cells(0, 10, 2)
+    # state tuning to a wanted flow (test_region_model_stacks.py:316-333)
+    q_avg = (model.statistics.discharge_value(cids, 10) + model.statistics.discharge_value(cids, 11)) / 2.0
+    x = 0.7
+    model.revert_to_initial_state()
+    s_before = [s.kirchner.q for s in model.current_state]
+    r = model.adjust_state_to_target_flow(x * q_avg, cids, start_step=10, scale_range=3.0, scale_eps=1e-3,
+                                          max_iter=350, n_steps=2)
+    assert len(r.diagnostics) == 0
+    assert r.q_r == pytest.approx(q_avg * x, abs=0.5e-2)
+    assert r.q_0 == pytest.approx(q_avg, abs=0.5e-2)
+    # the state left behind is the tuned one: a uniform scale of every selected cell's q
+    s_after = [s.kirchner.q for s in model.current_state]
+    ratio = np.array(s_after) / np.array(s_before)
+    assert np.allclose(ratio, ratio[0], rtol=1e-12) and 1 / 3 < ratio[0] < 3
+    model.run_cells(0, 10, 2)
+    q_tuned = (model.statistics.discharge_value(cids, 10) + model.statistics.discharge_value(cids, 11)) / 2.0
+    assert q_tuned == pytest.approx(r.q_r, rel=1e-12)
+    r = model.adjust_state_to_target_flow(float("nan"), cids, start_step=10, scale_range=3.0, scale_eps=1e-3,
+                                          max_iter=300, n_steps=2)
+    assert len(r.diagnostics) > 0
+    model.cells[0].env_ts.temperature.set(10, float("nan"))
+    r = model.adjust_state_to_target_flow(30.0, cids, start_step=10, scale_range=3.0, scale_eps=1e-3, max_iter=300,
+                                          n_steps=2)
+    assert len(r.diagnostics) > 0
 
 
 def test_run_cells_argument_errors():

@@ -98,3 +98,30 @@ def test_land_type_fractions_validation():
         f.set_fractions(glacier=0.5, lake=0.5, reservoir=0.5, forest=0.0)
     f.set_fractions(glacier=0.2, lake=0.2, reservoir=0.2, forest=0.4004)  # within 1e-3: normalised
     assert f.glacier() + f.lake() + f.reservoir() + f.forest() == pytest.approx(1.0)
+
+
+def test_find_min_single_variable():
+    """The state tuner's 1-D minimiser (restated dlib::find_min_single_variable, host/optimize.hpp):
+    smooth and kinked minima, a minimum on the bound, the iteration cap and argument checks."""
+    calls = []
+
+    def quad(x):
+        calls.append(x)
+        return (x - 2.0) ** 2
+
+    x, fx = api.find_min_single_variable(quad, 1.0, 0.0, 5.0, 1e-6, 100)
+    assert abs(x - 2.0) < 1e-6 and fx < 1e-12
+    assert all(0.0 <= c <= 5.0 for c in calls)  # never evaluated outside [begin, end]
+    x, _ = api.find_min_single_variable(lambda x: abs(x - 3.3), 0.5, 0.0, 10.0, 1e-7, 200)
+    assert abs(x - 3.3) < 1e-6
+    x, _ = api.find_min_single_variable(lambda x: (x - 10.0) ** 2, 1.0, 0.0, 5.0, 1e-6, 200)
+    assert abs(x - 5.0) < 1e-5  # minimum pinned at the end bound
+    x, _ = api.find_min_single_variable(lambda x: (x - 0.7) ** 2, 0.3, 0.1, 0.9, 1e-9, 100, 0.05)
+    assert abs(x - 0.7) < 1e-8  # small search radius: bracket grows outward
+    with pytest.raises(RuntimeError, match="max number of iterations"):
+        api.find_min_single_variable(lambda x: math.cos(x) * x, 1.0, 0.0, 50.0, 1e-12, 4)
+    with pytest.raises(RuntimeError, match="invalid arguments"):
+        api.find_min_single_variable(quad, float("nan"), 0.0, 5.0)
+    with pytest.raises(RuntimeError):
+        api.find_min_single_variable(quad, 6.0, 0.0, 5.0)
+    assert api.FlowAdjustResult().diagnostics == ""
