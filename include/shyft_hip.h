@@ -158,6 +158,11 @@ int shyft_hip_statistics(const shyft_hip_region* h, int series, const int64_t* i
  * region_model.h:873-885): dst[n_catchments][n] in catchment_ids() order, device or host. */
 int shyft_hip_catchment_sums(const shyft_hip_region* h, int series, size_t step0, size_t n, double* dst,
                              int dst_on_device);
+/* Per-catchment sums of value x cell area (calculated catchments, cell order, same reduction as
+ * shyft_hip_catchment_sums): the area-weighted snow sca/swe sums of the calibration goal function
+ * (optimizer::extract_area_ts_property, core/model_calibration.h:759-776). dst[n_catchments][n]. */
+int shyft_hip_catchment_area_sums(const shyft_hip_region* h, int series, size_t step0, size_t n, double* dst,
+                                  int dst_on_device);
 size_t shyft_hip_number_of_catchments(const shyft_hip_region* h);
 int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids);
 

@@ -49,6 +49,7 @@ SIGNATURES = {
     "shyft_hip_statistics": (C.c_int, [_h, C.c_int, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_size_t, C.c_size_t,
                                        C.c_void_p]),
     "shyft_hip_catchment_sums": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
+    "shyft_hip_catchment_area_sums": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
     "shyft_hip_number_of_catchments": (C.c_size_t, [_h]),
     "shyft_hip_catchment_ids": (C.c_int, [_h, C.c_void_p]),
     "shyft_hip_region_clone": (C.c_int, [_h, C.POINTER(C.c_void_p)]),

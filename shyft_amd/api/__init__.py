@@ -82,7 +82,9 @@ class _Vector(list):
 
 
 class IntVector(_Vector):
-    pass
+    @staticmethod
+    def from_numpy(a):
+        return IntVector(int(x) for x in np.asarray(a))
 
 
 class DoubleVector(_Vector):
@@ -112,10 +114,16 @@ class stat_scope:  # core/cell_model.h:183-186
 class TimeSeries:
     """A point series on a fixed_dt or point time axis (the apoint_ts results of the statistics)."""
 
-    def __init__(self, ta=None, values=None, point_fx=POINT_AVERAGE_VALUE, _impl=None):
+    def __init__(self, ta=None, values=None, point_fx=POINT_AVERAGE_VALUE, _impl=None, fill_value=None):
         if _impl is not None:
             self._ts = _impl
             return
+        if isinstance(ta, TimeSeries):  # copy constructor
+            import copy
+            self._ts = copy.deepcopy(ta._ts)
+            return
+        if values is None and fill_value is not None:
+            values = float(fill_value)
         if isinstance(values, (int, float)):
             values = [float(values)] * ta.size()
         self._ts = _api._PointTs(ta, [float(v) for v in np.asarray(values, dtype=np.float64)], point_fx)
@@ -634,3 +642,14 @@ class _RiverNetworkProxy:
             self._m._river_network = rn2
             return self if r is rn2 else r
         return call
+
+
+# ---- calibration (model_calibration.h; expose.h:472-730) -------------------------------------------------------------
+from ._calibration import (  # noqa: E402,F401
+    NASH_SUTCLIFFE, KLING_GUPTA, ABS_DIFF, RMSE, DISCHARGE, SNOW_COVERED_AREA, SNOW_WATER_EQUIVALENT,
+    ROUTED_DISCHARGE, CELL_CHARGE, TsTransform, TargetSpecificationPts, TargetSpecificationVector,
+)
+from ._api import (  # noqa: E402,F401
+    nash_sutcliffe_goal_function, kling_gupta_goal_function, rmse_goal_function, abs_diff_sum_goal_function,
+    abs_diff_sum_goal_function_scaled,
+)

@@ -143,3 +143,14 @@ def create_opt_model_clone(src_model):
 
 def create_full_model_clone(src_model):
     return HbvModel(src_model)
+
+
+# the model types know their optimizer, parameter and state types (expose.h:147-170, model_calibrator)
+from .._calibration import make_optimizer_type  # noqa: E402
+
+HbvOptimizer = make_optimizer_type("HbvOptimizer", _api._HbvOptimizer)
+for _m in (HbvModel, HbvOptModel):
+    _m.optimizer_t = HbvOptimizer
+    _m.parameter_t = _HbvBase._parameter_t
+    _m.state_t = _HbvBase._state_t
+del _m

@@ -123,3 +123,14 @@ def create_full_model_clone(src_model, with_catchment_params=False):
         for cid in list(m._catchment_parameters):
             m.remove_catchment_parameter(cid)
     return m
+
+
+# the model types know their optimizer, parameter and state types (expose.h:147-170, model_calibrator)
+from .._calibration import make_optimizer_type  # noqa: E402
+
+PTGSKOptimizer = make_optimizer_type("PTGSKOptimizer", _api._PTGSKOptimizer)
+for _m in (PTGSKModel, PTGSKOptModel):
+    _m.optimizer_t = PTGSKOptimizer
+    _m.parameter_t = _PTGSKBase._parameter_t
+    _m.state_t = _PTGSKBase._state_t
+del _m

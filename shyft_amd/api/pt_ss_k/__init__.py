@@ -102,3 +102,14 @@ def create_opt_model_clone(src_model):
 
 def create_full_model_clone(src_model):
     return PTSSKModel(src_model)
+
+
+# the model types know their optimizer, parameter and state types (expose.h:147-170, model_calibrator)
+from .._calibration import make_optimizer_type  # noqa: E402
+
+PTSSKOptimizer = make_optimizer_type("PTSSKOptimizer", _api._PTSSKOptimizer)
+for _m in (PTSSKModel, PTSSKOptModel):
+    _m.optimizer_t = PTSSKOptimizer
+    _m.parameter_t = _PTSSKBase._parameter_t
+    _m.state_t = _PTSSKBase._state_t
+del _m

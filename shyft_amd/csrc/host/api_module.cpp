@@ -16,6 +16,7 @@
 
 #include <cmath>
 
+#include "calibration.hpp"
 #include "region_model.hpp"
 
 namespace py = pybind11;
@@ -101,6 +102,41 @@ void bind_model(py::module_& m, const char* name) {
         .def("_river_output_flow_m3s", &M::river_output_flow_m3s)
         .def("_river_upstream_inflow_m3s", &M::river_upstream_inflow_m3s)
         .def("_river_local_inflow_m3s", &M::river_local_inflow_m3s);
+}
+
+// model_calibration::optimizer<region_model> (expose.h:472-730 model_calibrator)
+template <class Stack>
+void bind_optimizer(py::module_& m, const char* name) {
+    using M = region_model<Stack>;
+    using O = optimizer<M>;
+    py::class_<O>(m, name)
+        .def(py::init<M&, const std::vector<target_specification>&, const std::vector<double>&, const std::vector<double>&>(),
+             py::arg("model"), py::arg("targets"), py::arg("p_min"), py::arg("p_max"), py::keep_alive<1, 2>())
+        .def(py::init<M&>(), py::arg("model"), py::keep_alive<1, 2>())
+        .def("_set_target_specification", &O::set_target_specification)
+        .def("_set_parameter_ranges", &O::set_parameter_ranges)
+        .def_readwrite("_targets", &O::targets)
+        .def_readwrite("_lower", &O::parameter_lower_bound)
+        .def_readwrite("_upper", &O::parameter_upper_bound)
+        .def_readwrite("batch_evaluation", &O::batch_evaluation)
+        .def_readwrite("max_batch_members", &O::max_batch_members)
+        .def("establish_initial_state_from_model", &O::establish_initial_state_from_model)
+        .def("_get_initial_state", &O::get_initial_state)
+        .def("set_verbose_level", &O::set_verbose_level, py::arg("level"))
+        .def("reset_states", &O::reset_states)
+        .def("parameter_active", &O::active_parameter, py::arg("i"))
+        .def_property_readonly("trace_size", &O::trace_size)
+        .def_readonly("trace_goal_function_values", &O::goal_fn_trace)
+        .def("trace_goal_function_value", &O::trace_goal_fn, py::arg("i"))
+        .def("_trace_parameter", &O::trace_parameter)
+        .def("_calculate_goal_function", &O::calculate_goal_function, py::call_guard<py::gil_scoped_release>())
+        .def("_calculate_goal_functions", &O::calculate_goal_functions, py::call_guard<py::gil_scoped_release>())
+        .def("_optimize", &O::optimize, py::call_guard<py::gil_scoped_release>())
+        .def("_optimize_global", &O::optimize_global, py::call_guard<py::gil_scoped_release>())
+        .def("_optimize_sceua", &O::optimize_sceua, py::call_guard<py::gil_scoped_release>())
+        .def("_optimize_dream", &O::optimize_dream, py::call_guard<py::gil_scoped_release>())
+        .def("_to_scaled", &O::to_scaled)
+        .def("_from_scaled", &O::from_scaled);
 }
 
 }  // namespace
@@ -304,6 +340,78 @@ PYBIND11_MODULE(_api, m) {
     bind_model<pt_gs_k_stack>(m, "_PTGSKRegionModel");
     bind_model<hbv_stack_stack>(m, "_HbvRegionModel");
     bind_model<pt_ss_k_stack>(m, "_PTSSKRegionModel");
+
+    py::enum_<target_spec_calc_type>(m, "target_spec_calc_type")
+        .value("NASH_SUTCLIFFE", NASH_SUTCLIFFE)
+        .value("KLING_GUPTA", KLING_GUPTA)
+        .value("ABS_DIFF", ABS_DIFF)
+        .value("RMSE", RMSE)
+        .export_values();
+    py::enum_<target_property_type>(m, "target_property_type")
+        .value("DISCHARGE", DISCHARGE)
+        .value("SNOW_COVERED_AREA", SNOW_COVERED_AREA)
+        .value("SNOW_WATER_EQUIVALENT", SNOW_WATER_EQUIVALENT)
+        .value("ROUTED_DISCHARGE", ROUTED_DISCHARGE)
+        .value("CELL_CHARGE", CELL_CHARGE)
+        .export_values();
+    py::class_<target_specification>(m, "_TargetSpecification")
+        .def(py::init<>())
+        .def_readwrite("ts", &target_specification::ts)
+        .def_readwrite("catchment_indexes", &target_specification::catchment_indexes)
+        .def_readwrite("river_id", &target_specification::river_id)
+        .def_readwrite("scale_factor", &target_specification::scale_factor)
+        .def_readwrite("calc_mode", &target_specification::calc_mode)
+        .def_readwrite("catchment_property", &target_specification::catchment_property)
+        .def_readwrite("s_r", &target_specification::s_r)
+        .def_readwrite("s_a", &target_specification::s_a)
+        .def_readwrite("s_b", &target_specification::s_b)
+        .def_readwrite("uid", &target_specification::uid);
+    // goal functions on value vectors (time_series.h:2301-2450), for tests and direct use
+    m.def("nash_sutcliffe_goal_function", &goal::nash_sutcliffe, py::arg("observed"), py::arg("model"));
+    m.def("kling_gupta_goal_function", &goal::kling_gupta, py::arg("observed"), py::arg("model"), py::arg("s_r"),
+          py::arg("s_a"), py::arg("s_b"));
+    m.def("rmse_goal_function", &goal::rmse, py::arg("observed"), py::arg("model"));
+    m.def("abs_diff_sum_goal_function", &goal::abs_diff_sum, py::arg("observed"), py::arg("model"));
+    m.def("abs_diff_sum_goal_function_scaled", &goal::abs_diff_sum_scaled, py::arg("observed"), py::arg("model"),
+          py::arg("scale"));
+    m.def("_average_onto", &average_onto);
+    // search algorithms over a Python callable (scaled space [0,1]^n), for tests of the restatements
+    m.def("_sceua_find_min", [](const std::function<double(const std::vector<double>&)>& f, std::vector<double> x,
+                                size_t max_n, double x_eps, double y_eps) {
+        const size_t n = x.size();
+        std::vector<double> lo(n, 0.0), hi(n, 1.0), xe(n, x_eps);
+        scaled_fx fx{f, [&f](const std::vector<std::vector<double>>& xs) {
+                         std::vector<double> r;
+                         for (const auto& v : xs) r.push_back(f(v));
+                         return r;
+                     }};
+        double y = 0;
+        auto st = sceua_search().find_min(lo, hi, x, y, fx, y_eps, -1.0, -2.0, xe, max_n, false);
+        return std::make_tuple(x, y, int(st));
+    });
+    m.def("_dream_find_max", [](const std::function<double(const std::vector<double>&)>& f, std::vector<double> x,
+                                size_t max_n) {
+        scaled_fx fx{f, [&f](const std::vector<std::vector<double>>& xs) {
+                         std::vector<double> r;
+                         for (const auto& v : xs) r.push_back(f(v));
+                         return r;
+                     }};
+        double y = dream_search().find_max(fx, x, max_n, false);
+        return std::make_pair(x, y);
+    });
+    m.def("_box_trust_region_min", [](const std::function<double(const std::vector<double>&)>& f, std::vector<double> x,
+                                      double rho_begin, double rho_end, size_t max_n) {
+        scaled_fx fx{f, [&f](const std::vector<std::vector<double>>& xs) {
+                         std::vector<double> r;
+                         for (const auto& v : xs) r.push_back(f(v));
+                         return r;
+                     }};
+        auto r = box_trust_region::minimize(fx, x, rho_begin, rho_end, max_n);
+        return std::make_tuple(r.x, r.f, r.evaluations);
+    });
+    bind_optimizer<pt_gs_k_stack>(m, "_PTGSKOptimizer");
+    bind_optimizer<hbv_stack_stack>(m, "_HbvOptimizer");
+    bind_optimizer<pt_ss_k_stack>(m, "_PTSSKOptimizer");
 
     py::register_exception_translator([](std::exception_ptr p) {
         try {

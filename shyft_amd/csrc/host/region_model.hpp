@@ -644,6 +644,51 @@ class region_model {
         }
         return r;
     }
+    // per-catchment sums of value x cell area: [catchment][t], calculated catchments only (others 0)
+    std::vector<std::vector<double>> catchment_area_sums(int series) const {
+        const size_t C = number_of_catchments(), T = time_axis.size();
+        std::vector<double> flat(C * T);
+        throw_if(shyft_hip_catchment_area_sums(h_.get(), series, 0, T, flat.data(), 0), h_.get());
+        std::vector<std::vector<double>> r(C);
+        for (size_t c = 0; c < C; ++c) {
+            if (catchment_filter_.empty() || catchment_filter_[c]) r[c].assign(flat.begin() + c * T, flat.begin() + (c + 1) * T);
+            else r[c].assign(T, 0.0);
+        }
+        return r;
+    }
+    bool is_calculated_by_catchment_ix(size_t cix) const { return catchment_filter_.empty() || catchment_filter_.at(cix); }
+    size_t cix_from_cid(int64_t cid) const {
+        auto f = cid_to_cix_.find(cid);
+        if (f == cid_to_cix_.end()) throw std::runtime_error("region_model: no match for cid in map lookup");
+        return f->second;
+    }
+    size_t catchment_ix_of_cell(size_t i) const { return cid_to_cix_.at(geo_.at(i).catchment_id()); }
+
+    // ---- parameter ensembles (shyft_hip_ensemble_run): every member runs the calculated cells over the whole
+    // time axis from the CURRENT state with its own region parameter vector; the model's own state/responses
+    // are untouched. collect_snow adds the snow sca/swe series (2, 3).
+    void ensemble_run(const std::vector<parameter_t>& members, bool collect_snow) {
+        if (members.empty()) throw std::runtime_error("ensemble_run: no members");
+        const size_t w = members[0].size();
+        std::vector<double> flat;
+        flat.reserve(members.size() * w);
+        for (const auto& p : members) {
+            check_param(p);
+            if (p.size() != w) throw std::runtime_error(Stack::param_error);
+            flat.insert(flat.end(), p.begin(), p.end());
+        }
+        throw_if(shyft_hip_ensemble_run(h_.get(), flat.data(), members.size(), w, 0, int(time_axis.size()),
+                                        collect_snow ? SHYFT_HIP_COLLECT_DISCHARGE_SNOW : SHYFT_HIP_COLLECT_DISCHARGE),
+                 h_.get());
+        ens_members_ = members.size();
+    }
+    // [member][catchment][t] sums (area_weighted: of value x cell area) of the last ensemble run
+    std::vector<double> ensemble_sums(int series, bool area_weighted) const {
+        const size_t C = number_of_catchments(), T = time_axis.size();
+        std::vector<double> flat(ens_members_ * C * T);
+        throw_if(shyft_hip_ensemble_sums(h_.get(), series, area_weighted ? 1 : 0, 0, T, flat.data(), 0), h_.get());
+        return flat;
+    }
 
     // ---- routing (region_model.h:424-440, 906-949; core/routing.h)
     void connect_catchment_to_river(int64_t cid, int64_t rid) {
@@ -682,6 +727,7 @@ class region_model {
     std::vector<bool> catchment_filter_;
     std::vector<bool> state_collection_, snow_collection_;
     mutable bool routing_dirty_ = true;
+    size_t ens_members_ = 0;
 
     static double pot_ratio(double q_m3s, double area_m2, double scale_factor) {
         const double water_level = q_m3s * (3600.0 * 1000.0) / area_m2;  // m3s_to_mmh (unit_conversion.h:12-15)

@@ -1012,6 +1012,27 @@ int shyft_hip_catchment_sums(const shyft_hip_region* hc, int series, size_t step
     });
 }
 
+int shyft_hip_catchment_area_sums(const shyft_hip_region* hc, int series, size_t step0, size_t n, double* dst,
+                                  int dst_on_device) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_catchment_area_sums: null argument");
+    return guarded(h, [&] {
+        const double* src = series_rows(h, series, step0, n, "catchment_area_sums");
+        update_derived(h);  // per-cell constants (cell area) are current
+        const size_t C = h->cix_to_cid.size();
+        const double* w = h->d_cellc.p + size_t(h->hbv() ? HC_AREA : PC_AREA) * h->n;
+        double* out = dst;
+        if (!dst_on_device) {
+            h->d_tmp.alloc(std::max(h->d_tmp.n, C * n));
+            out = h->d_tmp.p;
+        }
+        hip_check(launch_segment_sums(src, h->n, n, h->d_seg_cells.p, h->d_seg_off.p, C, out, h->stream, w),
+                  "segment_sums");
+        if (!dst_on_device) copy_rows(h->stream, dst, out, C * n * sizeof(double), 0, 1);
+        else hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
 size_t shyft_hip_number_of_catchments(const shyft_hip_region* h) { return h ? h->cix_to_cid.size() : 0; }
 
 int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids) {
