@@ -126,6 +126,27 @@ int shyft_hip_get_forcing(const shyft_hip_region* h, int var, size_t step0, size
 int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const double* src_xyz,
                           const double* src_values, size_t step0, size_t n, const double* idw_param);
 
+/* Bayesian temperature kriging of the temperature forcing into the calculated cells, steps [step0, step0+n)
+ * of the resident window: region_model::interpolate's default temperature method
+ * (core/region_model.h:460-468 -> bayesian_kriging::btk_interpolation, core/bayesian_kriging.h:280-402).
+ *  src_xyz        : n_sources x 3
+ *  src_values     : [n][n_sources] on the model axis (average_accessor is the caller's); NaN = missing, and
+ *                   a step whose valid-source set differs from the full set uses the reference's reduced
+ *                   operators for that set
+ *  prior_gradient : [n] the prior temperature gradient per step (parameter.temperature_gradient(period)), or
+ *                   NULL for bayesian_kriging::parameter's day-of-year formula on the region's time axis
+ *                   (bayesian_kriging.h:220-223)
+ *  btk_param      : temperature_gradient_sd (C/m, i.e. already /100), sill, nugget, range, zscale
+ * One source is copied to the cells (region_model.h:470-481). Errors carry the reference's texts ("needs at
+ * least two sources at different heights", "No valid sources for time period"). */
+int shyft_hip_interpolate_btk(shyft_hip_region* h, size_t n_sources, const double* src_xyz, const double* src_values,
+                              size_t step0, size_t n, const double* prior_gradient, const double* btk_param);
+/* Stateless bayesian_kriging_temperature (api/boostpython/api_interpolation.cpp:54-71) on a device (device < 0 =
+ * current): dst_xyz [n_dst][3], prior_gradient [n] (required), out [n][n_dst] host. */
+int shyft_hip_btk(int device, size_t n_sources, const double* src_xyz, const double* src_values, size_t n,
+                  const double* prior_gradient, const double* btk_param, size_t n_dst, const double* dst_xyz,
+                  double* out);
+
 /* Deterministic synthetic forcing for steps [step0, step0+n) of the resident window,
  * generated on device (bench/test workload; SURVEY.md §8d generator). */
 int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n);

@@ -442,3 +442,36 @@ extern "C" void oracle_make_uhg(int n_steps, double alpha, double beta, double* 
     std::copy(w.begin(), w.end(), out);
     *len = int(w.size());
 }
+
+// ---- Bayesian temperature kriging (core/bayesian_kriging.h:280-402) -------------------------------------------------
+#include "btk.hpp"
+
+// param: gradient_sd (already /100), sill, nugget, range, zscale. src_values [T][S], prior_gradient [T], out [T][D].
+extern "C" int oracle_btk_run(size_t S, const double* src_xyz, const double* src_values, size_t T,
+                              const double* prior_gradient, const double* param, size_t D, const double* dst_xyz,
+                              double* out, char* err, size_t errlen) {
+    btk::parameter p;
+    p.gradient_sd = param[0];
+    p.sill = param[1];
+    p.nug = param[2];
+    p.range = param[3];
+    p.zscale = param[4];
+    try {
+        btk::run(S, src_xyz, src_values, T, prior_gradient, p, D, dst_xyz, out);
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
+// the source-source covariance matrix K (utils::build_covariance_matrices, bayesian_kriging.h:93-113), out [S][S]
+extern "C" void oracle_btk_source_covariance(size_t S, const double* xyz, const double* param, double* out) {
+    btk::parameter p;
+    p.gradient_sd = param[0];
+    p.sill = param[1];
+    p.nug = param[2];
+    p.range = param[3];
+    p.zscale = param[4];
+    const auto K = btk::source_covariance(S, xyz, p);
+    std::copy(K.a.begin(), K.a.end(), out);
+}

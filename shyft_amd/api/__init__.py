@@ -21,7 +21,7 @@ from ._api import (  # noqa: F401  (re-exported names)
     GeoPoint, LandTypeFractions, RoutingInfo, GeoCellData, TimeAxisFixedDeltaT, point_interpretation_policy,
     POINT_INSTANT_VALUE, POINT_AVERAGE_VALUE, IDWParameter, IDWTemperatureParameter, IDWPrecipitationParameter,
     InterpolationParameter, UHGParameter, River, RiverNetwork, make_uhg_from_gamma, average_values, FlowAdjustResult,
-    find_min_single_variable,
+    find_min_single_variable, BTKParameter,
 )
 from . import _api
 
@@ -240,6 +240,22 @@ class WindSpeedSourceVector(_SourceVector):
 
 class RelHumSourceVector(_SourceVector):
     pass
+
+
+class GeoPointVector(_Vector):
+    pass
+
+
+def bayesian_kriging_temperature(src, dst, time_axis, btk_parameter):
+    """Bayesian temperature kriging of the sources onto the destination points over time_axis
+    (api/boostpython/api_interpolation.cpp:54-71), computed on the MI355X (shyft_hip_btk).
+    Returns a TemperatureSourceVector, one source per destination point."""
+    values = _api._bayesian_kriging_temperature([s._impl() for s in (src or [])], list(dst or []), time_axis,
+                                                btk_parameter)
+    out = TemperatureSourceVector()
+    for d, gp in enumerate(dst):
+        out.append(TemperatureSource(gp, TimeSeries(time_axis, values[:, d], POINT_AVERAGE_VALUE)))
+    return out
 
 
 class ARegionEnvironment:

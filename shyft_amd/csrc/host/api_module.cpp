@@ -282,8 +282,72 @@ PYBIND11_MODULE(_api, m) {
              }),
              py::arg("scale_factor") = 1.02, py::arg("max_members") = 20, py::arg("max_distance") = 200000.0)
         .def_readwrite("scale_factor", &idw_precipitation_parameter::scale_factor);
+    // BTKParameter (api/boostpython/api_interpolation.cpp:188-200)
+    py::class_<btk_parameter>(m, "BTKParameter")
+        .def(py::init<>())
+        .def(py::init<double, double>(), py::arg("temperature_gradient"), py::arg("temperature_gradient_sd"))
+        .def(py::init<double, double, double, double, double, double>(), py::arg("temperature_gradient"),
+             py::arg("temperature_gradient_sd"), py::arg("sill"), py::arg("nugget"), py::arg("range"), py::arg("zscale"))
+        .def("temperature_gradient", [](const btk_parameter& p, std::pair<double, double> period) {
+                 return p.temperature_gradient(utcperiod(to_us(period.first), to_us(period.second)));
+             }, py::arg("p"))
+        .def("temperature_gradient_sd", &btk_parameter::temperature_gradient_sd)
+        .def("sill", &btk_parameter::sill)
+        .def("nug", &btk_parameter::nug)
+        .def("range", &btk_parameter::range)
+        .def("zscale", &btk_parameter::zscale);
+    // bayesian_kriging_temperature (api_interpolation.cpp:54-71): validation, sources averaged onto the axis,
+    // one source copied, else the device BTK
+    m.def("_bayesian_kriging_temperature", [](const std::vector<geo_point_ts>& src, const std::vector<geo_point>& dst,
+                                              const fixed_dt& ta, const btk_parameter& p) {
+        if (src.empty() || dst.empty())
+            throw std::runtime_error("the supplied src and dst_points should be non-null and have at least one time-series");
+        if (ta.size() == 0 || ta.dt == 0)
+            throw std::runtime_error("the supplied destination time-axis should have more than 0 element, and a delta-t larger than 0");
+        const size_t S = src.size(), T = ta.size(), D = dst.size();
+        std::vector<double> xyz(3 * S), vals(T * S), prior(T), prm(5), dxyz(3 * D), out(T * D);
+        for (size_t s = 0; s < S; ++s) {
+            xyz[3 * s] = src[s].mid_point.x;
+            xyz[3 * s + 1] = src[s].mid_point.y;
+            xyz[3 * s + 2] = src[s].mid_point.z;
+            auto v = average_values(src[s].ts, ta);
+            for (size_t t = 0; t < T; ++t) vals[t * S + s] = v[t];
+        }
+        for (size_t d = 0; d < D; ++d) {
+            dxyz[3 * d] = dst[d].x;
+            dxyz[3 * d + 1] = dst[d].y;
+            dxyz[3 * d + 2] = dst[d].z;
+        }
+        for (size_t t = 0; t < T; ++t) prior[t] = p.temperature_gradient(ta.period(t));
+        p.as_abi(prm.data());
+        {
+            py::gil_scoped_release nogil;
+            throw_if(shyft_hip_btk(-1, S, xyz.data(), vals.data(), T, prior.data(), prm.data(), D, dxyz.data(),
+                                   out.data()),
+                     nullptr);
+        }
+        return py::array_t<double>({T, D}, out.data());
+    });
     py::class_<interpolation_parameter>(m, "InterpolationParameter")
         .def(py::init<>())
+        .def(py::init([](const btk_parameter& t, const idw_precipitation_parameter& p, const idw_parameter& ws,
+                         const idw_parameter& rad, const idw_parameter& rh) {
+                 interpolation_parameter ip;
+                 ip.temperature = t; ip.precipitation = p; ip.wind_speed = ws; ip.radiation = rad; ip.rel_hum = rh;
+                 return ip;
+             }),
+             py::arg("temperature"), py::arg("precipitation"), py::arg("wind_speed"), py::arg("radiation"),
+             py::arg("rel_hum"))
+        .def(py::init([](const idw_temperature_parameter& t, const idw_precipitation_parameter& p, const idw_parameter& ws,
+                         const idw_parameter& rad, const idw_parameter& rh) {
+                 interpolation_parameter ip;
+                 ip.temperature_idw = t; ip.use_idw_for_temperature = true;  // api_interpolation.cpp:447
+                 ip.precipitation = p; ip.wind_speed = ws; ip.radiation = rad; ip.rel_hum = rh;
+                 return ip;
+             }),
+             py::arg("temperature"), py::arg("precipitation"), py::arg("wind_speed"), py::arg("radiation"),
+             py::arg("rel_hum"))
+        .def_readwrite("temperature", &interpolation_parameter::temperature)
         .def_readwrite("use_idw_for_temperature", &interpolation_parameter::use_idw_for_temperature)
         .def_readwrite("temperature_idw", &interpolation_parameter::temperature_idw)
         .def_readwrite("precipitation", &interpolation_parameter::precipitation)

@@ -116,8 +116,31 @@ struct idw_precipitation_parameter : idw_parameter {
     double scale_factor = 1.02;
     idw_precipitation_parameter() { max_members = 20; }
 };
+// bayesian_kriging::parameter (core/bayesian_kriging.h:204-230): the prior gradient follows the day of year
+struct btk_parameter {
+    double gradient_sd = 0.0025, sill_value = 25.0, nug_value = 0.5, range_value = 200000.0, zscale_value = 20.0;
+    btk_parameter() = default;
+    btk_parameter(double /*temperature_gradient, not used*/, double temperature_gradient_sd)
+        : gradient_sd(temperature_gradient_sd / 100) {}
+    btk_parameter(double /*temperature_gradient*/, double temperature_gradient_sd, double sill, double nugget,
+                  double range, double zscale)
+        : gradient_sd(temperature_gradient_sd / 100), sill_value(sill), nug_value(nugget), range_value(range),
+          zscale_value(zscale) {}
+    double temperature_gradient(const utcperiod& p) const {
+        const double doy = double(day_of_year(p.start + (p.end - p.start) / 2));
+        return 1.18e-3 * std::sin(6.2831 / 365 * (doy + 79.0)) - 5.48e-3;
+    }
+    double temperature_gradient_sd() const { return gradient_sd; }
+    double sill() const { return sill_value; }
+    double nug() const { return nug_value; }
+    double range() const { return range_value; }
+    double zscale() const { return zscale_value; }
+    void as_abi(double* p) const { p[0] = gradient_sd; p[1] = sill_value; p[2] = nug_value; p[3] = range_value; p[4] = zscale_value; }
+};
+
 struct interpolation_parameter {
     bool use_idw_for_temperature = false;
+    btk_parameter temperature;
     idw_temperature_parameter temperature_idw;
     idw_precipitation_parameter precipitation;
     idw_parameter wind_speed, radiation, rel_hum;
@@ -332,10 +355,10 @@ class region_model {
         };
         guard([&] {
             if (env.temperature.empty()) return;
-            if (env.temperature.size() > 1 && !ip.use_idw_for_temperature)
-                throw std::runtime_error(
-                    "region_model::interpolate: bayesian kriging temperature interpolation is not part of the MI355X "
-                    "engine (set use_idw_for_temperature)");
+            if (env.temperature.size() > 1 && !ip.use_idw_for_temperature) {  // region_model.h:463-467
+                run_btk(env.temperature, ip.temperature);
+                return;
+            }
             const idw_temperature_parameter& t = ip.temperature_idw;
             run_idw(SHYFT_HIP_TEMPERATURE, env.temperature, t, t.default_temp_gradient, t.gradient_by_equation, 1.02);
         });
@@ -813,6 +836,23 @@ class region_model {
         const double prm[7] = {double(p.max_members), p.max_distance, p.distance_measure_factor, p.zscale,
                                gradient, by_eq ? 1.0 : 0.0, scale};
         throw_if(shyft_hip_interpolate(h_.get(), var, S, xyz.data(), vals.data(), 0, T, prm), h_.get());
+    }
+
+    // btk::btk_interpolation over the device (bayesian_kriging.h:280-402), sources averaged onto the axis
+    void run_btk(const std::vector<geo_point_ts>& src, const btk_parameter& p) {
+        const size_t S = src.size(), T = time_axis.size();
+        std::vector<double> xyz(3 * S), vals(T * S), prior(T), prm(5);
+        for (size_t s = 0; s < S; ++s) {
+            xyz[3 * s] = src[s].mid_point.x;
+            xyz[3 * s + 1] = src[s].mid_point.y;
+            xyz[3 * s + 2] = src[s].mid_point.z;
+            auto v = average_values(src[s].ts, time_axis);
+            for (size_t t = 0; t < T; ++t) vals[t * S + s] = v[t];
+        }
+        for (size_t t = 0; t < T; ++t) prior[t] = p.temperature_gradient(time_axis.period(t));
+        p.as_abi(prm.data());
+        throw_if(shyft_hip_interpolate_btk(h_.get(), S, xyz.data(), vals.data(), 0, T, prior.data(), prm.data()),
+                 h_.get());
     }
 
     // routing::model over the device (routing.h:239-387): which = 0 local_inflow, 1 upstream_inflow, 2 output_m3s

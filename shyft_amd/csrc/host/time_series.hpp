@@ -222,5 +222,20 @@ inline int64_t days_from_civil(int64_t y, int m, int d) {
 inline utctime utc_time(int64_t y, int mo, int d, int h = 0, int mi = 0, int s = 0, int us = 0) {
     return (days_from_civil(y, mo, d) * 86400 + int64_t(h) * 3600 + int64_t(mi) * 60 + s) * US + us;
 }
+// calendar::day_of_year (UTC): 1 + days since Jan 1 of t's year
+inline int day_of_year(utctime t) {
+    const int64_t day_us = int64_t(86400) * US;
+    int64_t days = t / day_us;
+    if (t % day_us != 0 && t < 0) --days;
+    int64_t z = days + 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    const int64_t doy_mar = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy_mar + 2) / 153;
+    const int m = int(mp < 10 ? mp + 3 : mp - 9);
+    const int64_t y = yoe + era * 400 + (m <= 2);
+    return int(1 + days - days_from_civil(y, 1, 1));
+}
 
 }  // namespace shyft_hip::host

@@ -153,3 +153,21 @@ hipError_t launch_idw_neighbours(const idw_nb_args& a, hipStream_t stream);
 hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream);
 hipError_t launch_copy_source(const double* v, int n_rows, int n_cells, const uint8_t* active, double* out,
                               hipStream_t stream);
+
+// Bayesian temperature kriging engine (kernels/btk.hip, core/bayesian_kriging.h:280-402). Host inputs are
+// read synchronously; the result is complete on `stream` when btk_run returns. Throws std::runtime_error
+// with the reference's messages.
+struct btk_args {
+    size_t n_sources;
+    const double* src_xyz;         // host [S][3]
+    const double* src_values;      // host [n_steps][S], NaN = missing
+    size_t n_steps;
+    const double* prior_gradient;  // host [n_steps]: parameter.temperature_gradient(period) per step
+    double gradient_sd, sill, nug, range, zscale;  // gradient_sd already /100 (bayesian_kriging.h:213-217)
+    size_t n_dst;
+    const double* d_dst_xyz;       // device [D][3]
+    const int32_t* d_dst_index;    // device [D] output column of each destination, or null (= d)
+    double* d_out;                 // device: step j, destination d -> d_out[j * ld_out + column]
+    size_t ld_out;
+};
+void btk_run(const btk_args& a, hipStream_t stream);

@@ -83,6 +83,22 @@ int64_t days_from_civil(int64_t y, int m, int d) {
 }
 constexpr int64_t DAY_US = 86400LL * 1000000LL;
 
+// calendar::day_of_year (UTC, core/utctime_utilities.cpp:230-235)
+int day_of_year(int64_t t_us) {
+    const int64_t days = floor_div(t_us, DAY_US);
+    int64_t y;
+    int m, d;
+    civil_from_days(days, y, m, d);
+    return int(1 + days - days_from_civil(y, 1, 1));
+}
+
+// bayesian_kriging::parameter::temperature_gradient(period) (core/bayesian_kriging.h:220-223): the prior
+// gradient from the day of year of the period's midpoint
+double btk_prior_gradient(int64_t start_us, int64_t dt_us) {
+    const double doy = double(day_of_year(start_us + dt_us / 2));
+    return 1.18e-3 * std::sin(6.2831 / 365 * (doy + 79.0)) - 5.48e-3;
+}
+
 }  // namespace
 
 struct shyft_hip_region {
@@ -131,6 +147,9 @@ struct shyft_hip_region {
     } idw[N_FORCING];
     dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
     bool dst_dirty = true;
+    // Bayesian temperature kriging destinations (calculated cells) and their window columns
+    dbuf<double> d_btk_xyz;
+    dbuf<int32_t> d_btk_index;
 
     // routing groups (cells sharing river + UHG): segment tables for the group discharge sums
     dbuf<int32_t> d_rseg_cells, d_rseg_off;
@@ -779,6 +798,128 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
         hip_check(launch_idw_gather(g, h->stream), "idw_gather");
         hip_check(hipStreamSynchronize(h->stream), "idw");
     });
+}
+
+namespace {
+void check_btk_param(const double* p) {
+    if (!(p[0] > 0.0) || !std::isfinite(p[0])) throw std::runtime_error("btk: temperature_gradient_sd must be > 0");
+    if (!(p[3] > 0.0)) throw std::runtime_error("btk: range must be > 0");
+}
+}  // namespace
+
+int shyft_hip_interpolate_btk(shyft_hip_region* h, size_t n_sources, const double* src_xyz, const double* src_values,
+                              size_t step0, size_t n, const double* prior_gradient, const double* btk_param) {
+    if (!h || !src_xyz || !src_values || !btk_param) return fail(h, "shyft_hip_interpolate_btk: null argument");
+    return guarded(h, [&] {
+        if (!h->has_geo) throw std::runtime_error("interpolate: geo_cell_data not set");
+        if (n_sources == 0) throw std::runtime_error("interpolate: no sources");
+        check_window(h, step0, n, "interpolate_btk");
+        check_btk_param(btk_param);
+        const size_t N = h->n;
+        double* out = h->d_forcing.p + (size_t(FV_TEMPERATURE) * h->TW + (step0 - h->w0)) * N;
+        if (n_sources == 1) {  // one temperature source: copied to the cells (region_model.h:470-481)
+            const uint8_t* active = h->active.empty() ? nullptr : h->d_active.p;
+            h->d_src_vals.alloc(std::max(h->d_src_vals.n, n));
+            hip_check(hipMemcpyAsync(h->d_src_vals.p, src_values, n * sizeof(double), hipMemcpyHostToDevice, h->stream),
+                      "upload source values");
+            hip_check(launch_copy_source(h->d_src_vals.p, int(n), int(N), active, out, h->stream), "copy_source");
+            hip_check(hipStreamSynchronize(h->stream), "sync");
+            return;
+        }
+        std::vector<double> prior;
+        if (!prior_gradient) {
+            prior.resize(n);
+            for (size_t i = 0; i < n; ++i) prior[i] = btk_prior_gradient(h->t0 + int64_t(step0 + i) * h->dt, h->dt);
+            prior_gradient = prior.data();
+        }
+        // destinations: the calculated cells (region_model.h:420-423), written in place of the window
+        std::vector<double> xyz;
+        std::vector<int32_t> index;
+        xyz.reserve(3 * N);
+        for (size_t i = 0; i < N; ++i) {
+            if (!h->active.empty() && !h->active[i]) continue;
+            for (int k = 0; k < 3; ++k) xyz.push_back(h->geo[i * 11 + k]);
+            index.push_back(int32_t(i));
+        }
+        const size_t D = index.size();
+        if (D == 0) return;
+        h->d_btk_xyz.alloc(3 * D);
+        hip_check(hipMemcpyAsync(h->d_btk_xyz.p, xyz.data(), 3 * D * sizeof(double), hipMemcpyHostToDevice, h->stream),
+                  "upload btk destinations");
+        const bool all = D == N;
+        if (!all) {
+            h->d_btk_index.alloc(D);
+            hip_check(hipMemcpyAsync(h->d_btk_index.p, index.data(), D * sizeof(int32_t), hipMemcpyHostToDevice,
+                                     h->stream),
+                      "upload btk index");
+        }
+        btk_args a{};
+        a.n_sources = n_sources;
+        a.src_xyz = src_xyz;
+        a.src_values = src_values;
+        a.n_steps = n;
+        a.prior_gradient = prior_gradient;
+        a.gradient_sd = btk_param[0];
+        a.sill = btk_param[1];
+        a.nug = btk_param[2];
+        a.range = btk_param[3];
+        a.zscale = btk_param[4];
+        a.n_dst = D;
+        a.d_dst_xyz = h->d_btk_xyz.p;
+        a.d_dst_index = all ? nullptr : h->d_btk_index.p;
+        a.d_out = out;
+        a.ld_out = N;
+        btk_run(a, h->stream);
+        hip_check(hipStreamSynchronize(h->stream), "btk");
+    });
+}
+
+int shyft_hip_btk(int device, size_t n_sources, const double* src_xyz, const double* src_values, size_t n,
+                  const double* prior_gradient, const double* btk_param, size_t n_dst, const double* dst_xyz,
+                  double* out) {
+    if (!src_xyz || !src_values || !prior_gradient || !btk_param || !dst_xyz || !out)
+        return fail(nullptr, "shyft_hip_btk: null argument");
+    try {
+        if (n_sources == 0) throw std::runtime_error("bayesian_kriging_temperature: no sources");
+        check_btk_param(btk_param);
+        if (n == 0 || n_dst == 0) return 0;
+        if (n_sources == 1) {  // api_interpolation.cpp:63-69: a clean copy to the destinations
+            for (size_t t = 0; t < n; ++t)
+                for (size_t d = 0; d < n_dst; ++d) out[t * n_dst + d] = src_values[t];
+            return 0;
+        }
+        if (device >= 0) hip_check(hipSetDevice(device), "hipSetDevice");
+        hipStream_t s = nullptr;
+        hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+        std::unique_ptr<std::remove_pointer<hipStream_t>::type, void (*)(hipStream_t)> stream(
+            s, [](hipStream_t x) { (void)hipStreamDestroy(x); });
+        dbuf<double> d_xyz, d_out;
+        d_xyz.alloc(3 * n_dst);
+        d_out.alloc(n * n_dst);
+        hip_check(hipMemcpyAsync(d_xyz.p, dst_xyz, 3 * n_dst * sizeof(double), hipMemcpyHostToDevice, s), "upload");
+        btk_args a{};
+        a.n_sources = n_sources;
+        a.src_xyz = src_xyz;
+        a.src_values = src_values;
+        a.n_steps = n;
+        a.prior_gradient = prior_gradient;
+        a.gradient_sd = btk_param[0];
+        a.sill = btk_param[1];
+        a.nug = btk_param[2];
+        a.range = btk_param[3];
+        a.zscale = btk_param[4];
+        a.n_dst = n_dst;
+        a.d_dst_xyz = d_xyz.p;
+        a.d_dst_index = nullptr;
+        a.d_out = d_out.p;
+        a.ld_out = n_dst;
+        btk_run(a, s);
+        hip_check(hipMemcpyAsync(out, d_out.p, n * n_dst * sizeof(double), hipMemcpyDeviceToHost, s), "download");
+        hip_check(hipStreamSynchronize(s), "sync");
+        return 0;
+    } catch (const std::exception& e) {
+        return fail(nullptr, e.what());
+    }
 }
 
 int shyft_hip_synthetic_elevation(uint64_t seed, uint64_t cell_offset, size_t n_cells, double* z_host) {

@@ -127,6 +127,19 @@ class HipRegion:
         self._chk(self._L.shyft_hip_interpolate(self.h, var, xyz.shape[0], _ptr(xyz), _ptr(v), step0, v.shape[0],
                                                 _ptr(p)))
 
+    def interpolate_btk(self, src_xyz: np.ndarray, src_values: np.ndarray, step0: int, btk_param,
+                        prior_gradient=None):
+        """Bayesian temperature kriging into the temperature forcing (src_values [n][S] on the model axis).
+        btk_param: gradient_sd (C/m), sill, nugget, range, zscale; prior_gradient [n] or None (day-of-year prior)."""
+        xyz = np.ascontiguousarray(src_xyz, dtype=np.float64).reshape(-1, 3)
+        v = np.ascontiguousarray(src_values, dtype=np.float64).reshape(-1, xyz.shape[0])
+        p = np.ascontiguousarray(btk_param, dtype=np.float64)
+        assert p.size == 5
+        g = None if prior_gradient is None else np.ascontiguousarray(prior_gradient, dtype=np.float64)
+        assert g is None or g.size == v.shape[0]
+        self._chk(self._L.shyft_hip_interpolate_btk(self.h, xyz.shape[0], _ptr(xyz), _ptr(v), step0, v.shape[0],
+                                                    _ptr(g), _ptr(p)))
+
     def synthetic_forcing(self, seed: int, step0: int, n: int, cell_offset: int = 0):
         self._chk(self._L.shyft_hip_synthetic_forcing(self.h, seed, cell_offset, step0, n))
 
@@ -239,3 +252,18 @@ def route(group_sums, group_uhgs, group_river, river_uhgs, river_downstream, dev
     check(L.shyft_hip_route(device, G, T, src, on_dev, _ptr(gw), _ptr(glen), _ptr(gr), R, _ptr(rw), _ptr(rlen),
                             _ptr(rd), max_len, _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), 0), None)
     return tuple(out)
+
+
+def btk(src_xyz, src_values, prior_gradient, btk_param, dst_xyz, device: int = -1) -> np.ndarray:
+    """Stateless Bayesian temperature kriging on the device (shyft_hip_btk): src_values [n][S] on the model axis,
+    prior_gradient [n], btk_param (gradient_sd C/m, sill, nugget, range, zscale), dst_xyz [D][3] -> [n][D]."""
+    L = lib()
+    xyz = np.ascontiguousarray(src_xyz, dtype=np.float64).reshape(-1, 3)
+    v = np.ascontiguousarray(src_values, dtype=np.float64).reshape(-1, xyz.shape[0])
+    g = np.ascontiguousarray(prior_gradient, dtype=np.float64).reshape(v.shape[0])
+    p = np.ascontiguousarray(btk_param, dtype=np.float64).reshape(5)
+    d = np.ascontiguousarray(dst_xyz, dtype=np.float64).reshape(-1, 3)
+    out = np.empty((v.shape[0], d.shape[0]))
+    check(L.shyft_hip_btk(device, xyz.shape[0], _ptr(xyz), _ptr(v), v.shape[0], _ptr(g), _ptr(p), d.shape[0],
+                          _ptr(d), _ptr(out)), None)
+    return out
