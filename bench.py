@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--idw", action="store_true",
                     help="configs[2]: forcing interpolated each chunk by IDW from 500 stations (run_interpolation) "
                          "instead of the per-cell generator")
+    ap.add_argument("--btk", action="store_true",
+                    help="as --idw, but temperature by Bayesian kriging from the stations (the reference's default "
+                         "temperature method, region_model.h:460-468)")
     return ap.parse_args()
 
 
@@ -112,6 +115,12 @@ IDW_DEFAULTS = {
     3: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # rel_hum
     4: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],   # radiation
 }
+
+
+# bayesian_kriging::parameter() defaults (bayesian_kriging.h:204-217) in the C ABI layout:
+# gradient_sd [C/m], sill, nugget, range, zscale
+BTK_DEFAULTS = [0.0025, 25.0, 0.5, 200000.0, 20.0]
+FP64_PEAK_FLOPS = 78.6e12        # MI355X FP64 matrix/vector peak (AMD spec sheet; not in MI355X_MICROARCH.md)
 
 
 def dist_setup(n_gpus):
@@ -214,9 +223,9 @@ class Router:
         return self.out
 
 
-def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router=None):
+def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router=None, btk=False, btk_ms=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
-    or IDW from the station network), then run_cells (and the routing group sums)."""
+    or IDW / BTK from the station network), then run_cells (and the routing group sums)."""
     kernel_ms = []
     r.set_state(state0)
     for s in range(k_steps):
@@ -230,7 +239,13 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router
             xyz, vals = stations
             v = vals[s % len(vals)]
             for var in range(5):
-                r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
+                if var == 0 and btk:
+                    t = time.perf_counter()
+                    r.interpolate_btk(xyz, v[0], step0, BTK_DEFAULTS)   # synchronous
+                    if btk_ms is not None:
+                        btk_ms.append((time.perf_counter() - t) * 1e3)
+                else:
+                    r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
         r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
         if router is not None:
@@ -312,6 +327,8 @@ def main():
     state0 = stack_defaults(a.stack, cells)[1]
     read_b, write_b, state_b, kernel_name = STACKS[a.stack]
     stations = None
+    if a.btk:
+        a.idw = True
     if a.idw:
         # station series prepared on the host before timing (the reference's region_env input);
         # each step uploads its chunk (14.6 MB) and interpolates 5 variables on the GPU
@@ -323,10 +340,11 @@ def main():
 
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
-        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations, router)
+        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations, router, a.btk)
     barrier_sync(pg, local)
     t0 = time.perf_counter()
-    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations, router)
+    btk_ms = []
+    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations, router, a.btk, btk_ms)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
@@ -350,9 +368,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8d generator, seed 20251015; " +
-                ("500 stations, IDW per chunk)" if a.idw else "device-generated per chunk)"),
+                ("500 stations, BTK temperature + IDW per chunk)" if a.btk else
+                 "500 stations, IDW per chunk)" if a.idw else "device-generated per chunk)"),
         "config": {
-            "workload": (f"{a.stack} + inverse_distance from {N_STATIONS} stations, " if a.idw else f"{a.stack} ") +
+            "workload": (f"{a.stack} + bayesian kriging temperature + inverse_distance from {N_STATIONS} stations, "
+                         if a.btk else f"{a.stack} + inverse_distance from {N_STATIONS} stations, " if a.idw
+                         else f"{a.stack} ") +
                         f"region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
                         f"({a.steps} chunks of {chunk}), discharge_collector, default "
                         f"{dict(hbv_stack='HbvParameter', pt_ss_k='PTSSKParameter').get(a.stack, 'PTGSKParameter')}",
@@ -379,6 +400,20 @@ def main():
                     f"{state_b} B/cell state per launch (DESIGN.md)",
         },
     }
+    if a.btk:
+        # the BTK time loop per chunk: one fp64 GEMM [cells x (S+3)] x [(S+3) x chunk], plus host
+        # work (source rows, per-step beta); the full-set operators are built on the first chunk and reused
+        ms = max_over_ranks(pg, local, float(np.mean(btk_ms)))
+        flops = 2.0 * cells * (N_STATIONS + 3) * chunk
+        out["btk"] = {
+            "ms_per_chunk": ms,
+            "cell_steps_per_s": world * cells * chunk / (ms * 1e-3),
+            "roofline": {"bound": "fp64", "achieved": flops / (ms * 1e-3) / 1e12, "peak": FP64_PEAK_FLOPS / 1e12,
+                         "unit": "TFLOP/s", "frac": flops / (ms * 1e-3) / FP64_PEAK_FLOPS,
+                         "write_GBps": cells * chunk * 8 / (ms * 1e-3) / 1e9,
+                         "note": "2 * cells * (stations + 3) * chunk flops per call over its wall time "
+                                 "(host part included)"},
+        }
     if router is not None:
         o = router.out[2]
         out["config"]["workload"] += (f"; routing::uhg through a {len(router.rivers)}-river network "

@@ -157,7 +157,13 @@ hipError_t launch_copy_source(const double* v, int n_rows, int n_cells, const ui
 // Bayesian temperature kriging engine (kernels/btk.hip, core/bayesian_kriging.h:280-402). Host inputs are
 // read synchronously; the result is complete on `stream` when btk_run returns. Throws std::runtime_error
 // with the reference's messages.
+struct btk_cache;  // full-set operators + device A of the last call (kernels/btk.hip)
+btk_cache* btk_cache_create();
+void btk_cache_destroy(btk_cache* c);
+
 struct btk_args {
+    btk_cache* cache;              // or null (no reuse)
+    uint64_t dst_version;          // identifies the destination set for the cache; 0 = never reuse
     size_t n_sources;
     const double* src_xyz;         // host [S][3]
     const double* src_values;      // host [n_steps][S], NaN = missing

@@ -150,6 +150,10 @@ struct shyft_hip_region {
     // Bayesian temperature kriging destinations (calculated cells) and their window columns
     dbuf<double> d_btk_xyz;
     dbuf<int32_t> d_btk_index;
+    std::vector<double> btk_xyz_host;
+    std::vector<int32_t> btk_index_host;
+    uint64_t btk_dst_version = 0;
+    std::unique_ptr<btk_cache, void (*)(btk_cache*)> btk{nullptr, btk_cache_destroy};
 
     // routing groups (cells sharing river + UHG): segment tables for the group discharge sums
     dbuf<int32_t> d_rseg_cells, d_rseg_off;
@@ -843,17 +847,24 @@ int shyft_hip_interpolate_btk(shyft_hip_region* h, size_t n_sources, const doubl
         }
         const size_t D = index.size();
         if (D == 0) return;
-        h->d_btk_xyz.alloc(3 * D);
-        hip_check(hipMemcpyAsync(h->d_btk_xyz.p, xyz.data(), 3 * D * sizeof(double), hipMemcpyHostToDevice, h->stream),
-                  "upload btk destinations");
         const bool all = D == N;
-        if (!all) {
-            h->d_btk_index.alloc(D);
-            hip_check(hipMemcpyAsync(h->d_btk_index.p, index.data(), D * sizeof(int32_t), hipMemcpyHostToDevice,
-                                     h->stream),
-                      "upload btk index");
+        if (xyz != h->btk_xyz_host || index != h->btk_index_host || h->btk_dst_version == 0) {
+            h->d_btk_xyz.alloc(3 * D);
+            hip_check(hipMemcpy(h->d_btk_xyz.p, xyz.data(), 3 * D * sizeof(double), hipMemcpyHostToDevice),
+                      "upload btk destinations");
+            if (!all) {
+                h->d_btk_index.alloc(D);
+                hip_check(hipMemcpy(h->d_btk_index.p, index.data(), D * sizeof(int32_t), hipMemcpyHostToDevice),
+                          "upload btk index");
+            }
+            h->btk_xyz_host.swap(xyz);
+            h->btk_index_host.swap(index);
+            ++h->btk_dst_version;
         }
+        if (!h->btk) h->btk.reset(btk_cache_create());
         btk_args a{};
+        a.cache = h->btk.get();
+        a.dst_version = h->btk_dst_version;
         a.n_sources = n_sources;
         a.src_xyz = src_xyz;
         a.src_values = src_values;
