@@ -405,6 +405,69 @@ int oracle_hbv_run(size_t n_cells, const double* geo11, const double* params, co
     return 0;
 }
 
+// Run the pt_hs_k region model on the CPU with the reference scheduler.
+//  params    : n_sets x 18 (pt_hs_k.h:66-88 order); snow_dist : n_sets x 17 or null (default 5 bins)
+//  state     : n_cells x 20 in/out (pt_hs_k::FLAT order)
+//  out_main  : [2][T][n_cells]; out_full : [8][T][n_cells]; out_state : [19][T+1][n_cells]
+int oracle_pthsk_run(size_t n_cells, const double* geo11, const double* params, const double* snow_dist, size_t n_sets,
+                     const int32_t* set_ix, double* state, int64_t t0_us, int64_t dt_us, size_t T, int start_step,
+                     int n_steps, const double* temp, const double* prec, const double* ws, const double* rh,
+                     const double* rad, double* out_main, double* out_full, double* out_state, int ncore,
+                     double* elapsed_s, char* err, size_t errlen) {
+    try {
+        pthsk_region rm;
+        rm.time_axis = fixed_dt(t0_us, dt_us, T);
+        rm.params.resize(n_sets);
+        for (size_t k = 0; k < n_sets; ++k) {
+            rm.params[k].set(params + k * pt_hs_k::parameter::size());
+            auto sp = snow_param(nullptr, snow_dist ? snow_dist + k * 17 : nullptr);
+            rm.params[k].hs.s = sp.s;
+            rm.params[k].hs.intervals = sp.intervals;
+        }
+        rm.cells.resize(n_cells);
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.geo = geo_cell_data::from_raw(geo11 + i * 11);
+            int32_t k = set_ix ? set_ix[i] : 0;
+            if (k < 0 || size_t(k) >= n_sets) return fail(err, errlen, "oracle_pthsk_run: parameter set index out of range");
+            c.parameter = &rm.params[k];
+            c.state.set(state + i * pt_hs_k::FLAT);
+            c.temp.resize(T); c.prec.resize(T); c.ws.resize(T); c.rh.resize(T); c.rad.resize(T);
+            for (size_t t = 0; t < T; ++t) {
+                c.temp[t] = temp[t * n_cells + i];
+                c.prec[t] = prec[t * n_cells + i];
+                c.ws[t] = ws[t * n_cells + i];
+                c.rh[t] = rh[t * n_cells + i];
+                c.rad[t] = rad[t * n_cells + i];
+            }
+            c.col.full = out_full != nullptr;
+            c.col.collect_state = out_state != nullptr;
+        }
+        auto t_begin = std::chrono::steady_clock::now();
+        rm.run_cells(size_t(ncore < 0 ? 0 : ncore), start_step, n_steps);
+        auto t_end = std::chrono::steady_clock::now();
+        if (elapsed_s) *elapsed_s = std::chrono::duration<double>(t_end - t_begin).count();
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.state.get(state + i * pt_hs_k::FLAT);
+            for (size_t t = 0; t < T; ++t) {
+                if (out_main) {
+                    out_main[t * n_cells + i] = c.col.rc[pt_hs_k::AVG_DISCHARGE][t];
+                    out_main[(T + t) * n_cells + i] = c.col.rc[pt_hs_k::CHARGE_M3S][t];
+                }
+                if (out_full)
+                    for (int k = 0; k < pt_hs_k::N_ALL; ++k) out_full[(size_t(k) * T + t) * n_cells + i] = c.col.rc[k][t];
+            }
+            if (out_state)
+                for (size_t k = 0; k < pt_hs_k::N_SC; ++k)
+                    for (size_t t = 0; t <= T; ++t) out_state[(k * (T + 1) + t) * n_cells + i] = c.col.sc[k][t];
+        }
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
 }  // extern "C"
 
 // routing::model query (core/routing.h:347-387) for river `query`: local, upstream, output [T].

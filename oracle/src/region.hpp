@@ -14,6 +14,7 @@
 #include "hbv.hpp"
 #include "ptgsk.hpp"
 #include "ptssk.hpp"
+#include "pthsk.hpp"
 
 namespace oracle {
 
@@ -61,6 +62,21 @@ struct ptssk_cell {
         col.initialize(ta.size(), start_step, n_steps, geo.area);
         pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
         pt_ss_k::run_pt_ss_k(geo, *parameter, ta, start_step, n_steps, fv, state, col);
+    }
+};
+
+// pt_hs_k cell (pt_hs_k_cell_model.h:218-267)
+struct pthsk_cell {
+    geo_cell_data geo;
+    const pt_hs_k::parameter* parameter = nullptr;
+    pt_hs_k::state state;
+    std::vector<double> temp, prec, ws, rh, rad;
+    pt_hs_k::collectors col;
+    void run(const fixed_dt& ta, int start_step, int n_steps) {
+        if (parameter == nullptr) throw std::runtime_error("pt_hs_k::run with null parameter attempted");
+        col.initialize(ta.size(), start_step, n_steps, geo.area);
+        pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
+        pt_hs_k::run_pt_hs_k(geo, *parameter, ta, start_step, n_steps, fv, state, col);
     }
 };
 
@@ -127,5 +143,6 @@ struct region_of {
 using ptgsk_region = region_of<ptgsk_cell, pt_gs_k::parameter>;
 using hbv_region = region_of<hbv_cell, hbv_stack::parameter>;
 using ptssk_region = region_of<ptssk_cell, pt_ss_k::parameter>;
+using pthsk_region = region_of<pthsk_cell, pt_hs_k::parameter>;
 
 }  // namespace oracle

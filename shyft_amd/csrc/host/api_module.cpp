@@ -404,6 +404,7 @@ PYBIND11_MODULE(_api, m) {
     bind_model<pt_gs_k_stack>(m, "_PTGSKRegionModel");
     bind_model<hbv_stack_stack>(m, "_HbvRegionModel");
     bind_model<pt_ss_k_stack>(m, "_PTSSKRegionModel");
+    bind_model<pt_hs_k_stack>(m, "_PTHSKRegionModel");
 
     py::enum_<target_spec_calc_type>(m, "target_spec_calc_type")
         .value("NASH_SUTCLIFFE", NASH_SUTCLIFFE)
@@ -476,6 +477,7 @@ PYBIND11_MODULE(_api, m) {
     bind_optimizer<pt_gs_k_stack>(m, "_PTGSKOptimizer");
     bind_optimizer<hbv_stack_stack>(m, "_HbvOptimizer");
     bind_optimizer<pt_ss_k_stack>(m, "_PTSSKOptimizer");
+    bind_optimizer<pt_hs_k_stack>(m, "_PTHSKOptimizer");
 
     py::register_exception_translator([](std::exception_ptr p) {
         try {

@@ -197,6 +197,18 @@ struct pt_ss_k_stack {
     static constexpr const char* param_error = "pt_ss_k parameter accessor: .set size mismatch";
 };
 
+struct pt_hs_k_stack {
+    static constexpr int id = SHYFT_HIP_PT_HS_K;
+    static constexpr size_t n_param = 18;   // core/pt_hs_k.h:64 (+17 snow distribution values, optional)
+    static constexpr size_t n_state = 20;   // swe sca n_bins sp[8] sw[8] kirchner q
+    static constexpr size_t n_full_series = 8;
+    static constexpr int k_ae_scale = 3;
+    static constexpr int k_routing = 13;
+    static constexpr int state_q = 19;
+    static constexpr double q_min = 0.0;
+    static constexpr const char* param_error = "pt_ss_k parameter accessor: .set size missmatch";  // pt_hs_k.h:68
+};
+
 // ---- region_model ------------------------------------------------------------------------------------------------
 // result of adjust_state_to_target_flow (core/model_state_tuning.h:12-17)
 struct q_adjust_result {
@@ -265,6 +277,11 @@ class region_model {
             return {0.4, 0.1, 30000.0, 1.26, 0.0, 0.0, 0.0, 0.0, 0.1};
         if (Stack::id == SHYFT_HIP_PT_SS_K)  // skaugen::state() (skaugen.h:122-124) + kirchner::state()
             return {4.077, 40.77, 0.0, 0.0, 0.0, 0.0, 0.0, 0.1};
+        if (Stack::id == SHYFT_HIP_PT_HS_K) {  // hbv_snow::state() undistributed (hbv_snow.h:74-99) + kirchner::state()
+            state_t s(Stack::n_state, 0.0);
+            s[Stack::state_q] = 0.1;
+            return s;
+        }
         state_t s(Stack::n_state, 0.0);  // hbv_stack::state(): snow undistributed, soil sm 0, tank uz 20 lz 10
         s[3] = 20.0;                    // (hbv_soil.h:28, hbv_tank.h:32)
         s[4] = 10.0;
@@ -758,7 +775,8 @@ class region_model {
     }
 
     void check_param(const parameter_t& p) const {
-        if (p.size() != Stack::n_param && !(Stack::id == SHYFT_HIP_HBV_STACK && p.size() == Stack::n_param + 17))
+        const bool has_snow_dist = Stack::id == SHYFT_HIP_HBV_STACK || Stack::id == SHYFT_HIP_PT_HS_K;
+        if (p.size() != Stack::n_param && !(has_snow_dist && p.size() == Stack::n_param + 17))
             throw std::runtime_error(Stack::param_error);
     }
 

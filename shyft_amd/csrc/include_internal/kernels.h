@@ -72,6 +72,11 @@ struct ptssk_kargs {
 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream);
 
+// pt_hs_k (kernels/pthsk.hip): same arguments; params [n_sets][PTHSK_NP], state [PTHSK_NS][N],
+// state_series [PTHSK_NSC][win_len+1][N]
+using pthsk_kargs = ptssk_kargs;
+hipError_t launch_pthsk_run(const pthsk_kargs& a, hipStream_t stream);
+
 // routing (kernels/routing.hip): river aggregation of (river, UHG) group discharge sums
 struct routing_args {
     int n_steps, n_rivers, max_len;

@@ -98,6 +98,28 @@ enum ptssk_state_series_index {
 // per-cell constants: the pt_gs_k PC_* rows (pt_ss_k.h:237-245 are the same expressions)
 // response series: the pt_gs_k PR_* ids (snow_swe = snow_total_stored_water of the all-collector)
 
+// ------------------------------------------------------------------ pt_hs_k
+// parameter row: the 18 reference values in get/set order (core/pt_hs_k.h:66-88), then the hbv_snow
+// distribution (n_bins, s[HBV_MAX_BINS], intervals[HBV_MAX_BINS]) as for hbv_stack (hbv_snow.h:21-72)
+enum pthsk_param_index {
+    PH_C1 = 0, PH_C2, PH_C3, PH_AE_SCALE, PH_LW, PH_TX, PH_CX, PH_TS, PH_CFR, PH_DTF, PH_PCORR, PH_PT_ALBEDO,
+    PH_PT_ALPHA, PH_R_VELOCITY, PH_R_ALPHA, PH_R_BETA, PH_GM_DIRECT, PH_RSV_DRF,
+    PH_NB, PH_S0, PH_I0 = PH_S0 + HBV_MAX_BINS, PTHSK_NP = PH_I0 + HBV_MAX_BINS
+};
+#define PTHSK_NP_REF 18
+
+// pt_hs_k state (pt_hs_k.h:148-172): hbv_snow swe sca, the number of distributed bins (0 = not yet
+// distributed), the bins sp / sw, kirchner q
+enum pthsk_state_index {
+    PHS_SWE = 0, PHS_SCA, PHS_NB, PHS_SP0, PHS_SW0 = PHS_SP0 + HBV_MAX_BINS, PHS_KIRCHNER_Q = PHS_SW0 + HBV_MAX_BINS,
+    PTHSK_NS
+};
+// pt_hs_k state-collector series (pt_hs_k_cell_model.h:148-210): kirchner_discharge, snow_sca, snow_swe, sp[], sw[]
+enum pthsk_state_series_index {
+    PHC_KIRCHNER = 0, PHC_SCA, PHC_SWE, PHC_SP0, PHC_SW0 = PHC_SP0 + HBV_MAX_BINS, PTHSK_NSC = PHC_SW0 + HBV_MAX_BINS
+};
+// per-cell constants: the pt_gs_k PC_* rows (pt_hs_k.h:233-242 are the same expressions); response series: PR_*
+
 // per-cell error codes written by the stack kernels
 enum cell_error { ERR_NONE = 0, ERR_KIRCHNER_MAX_ITER = 1, ERR_NEGATIVE_OUTFLOW = 2, ERR_SKAUGEN_BISECT = 3,
                   ERR_SKAUGEN_PDF = 4 };

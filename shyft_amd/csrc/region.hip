@@ -168,15 +168,22 @@ struct shyft_hip_region {
 
     bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
     bool ptssk() const { return stack == SHYFT_HIP_PT_SS_K; }
+    bool pthsk() const { return stack == SHYFT_HIP_PT_HS_K; }
     size_t n_series() const {
         if (collect == COLLECT_ALL) return hbv() ? HBV_NR : PTGSK_NR;
         return collect == COLLECT_DISCHARGE_SNOW ? 4 : 2;
     }
-    size_t n_state_fields() const { return hbv() ? HBV_NS : (ptssk() ? PTSSK_NS : PTGSK_NS); }
+    size_t n_state_fields() const {
+        return hbv() ? HBV_NS : (ptssk() ? PTSSK_NS : (pthsk() ? PTHSK_NS : PTGSK_NS));
+    }
     // state-collector series per cell (pt_ss_k collects 7 series from its 8 state values)
-    size_t n_state_series() const { return ptssk() ? PTSSK_NSC : n_state_fields(); }
-    size_t n_ref_params() const { return hbv() ? HBV_NP_REF : (ptssk() ? PTSSK_NP : PTGSK_NP_REF); }
-    size_t param_width() const { return hbv() ? HBV_NP : (ptssk() ? PTSSK_NP : PTGSK_NP_REF); }
+    size_t n_state_series() const { return ptssk() ? PTSSK_NSC : (pthsk() ? PTHSK_NSC : n_state_fields()); }
+    size_t n_ref_params() const {
+        return hbv() ? HBV_NP_REF : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP_REF : PTGSK_NP_REF));
+    }
+    size_t param_width() const { return hbv() ? HBV_NP : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP : PTGSK_NP_REF)); }
+    // hbv_snow quantile distribution (n_bins, s[], intervals[]) in the parameter row, or -1
+    int snow_dist_index() const { return hbv() ? HK_NB : (pthsk() ? PH_NB : -1); }
 };
 
 namespace {
@@ -258,16 +265,19 @@ void update_derived_hbv(shyft_hip_region* h) {
     h->derived_dirty = false;
 }
 
-// pt_ss_k: parameter rows as given, per-cell constants of pt_ss_k.h:237-245 in the pt_gs_k PC_* rows
+// pt_ss_k / pt_hs_k: parameter rows as given, per-cell constants of pt_ss_k.h:237-245 (pt_hs_k.h:233-242,
+// the same expressions) in the pt_gs_k PC_* rows
 void update_derived_ptssk(shyft_hip_region* h) {
     const size_t N = h->n;
+    const size_t width = h->param_width();
+    const int k_gm = h->pthsk() ? PH_GM_DIRECT : SK_GM_DIRECT, k_rsv = h->pthsk() ? PH_RSV_DRF : SK_RSV_DRF;
     std::vector<double> cc(PTGSK_NC * N, 0.0);
     for (size_t i = 0; i < N; ++i) {
         const double* g = &h->geo[i * 11];
-        const double* p = &h->params[size_t(h->set_ix[i]) * PTSSK_NP];
+        const double* p = &h->params[size_t(h->set_ix[i]) * width];
         const double glacier = g[6], lake = g[7], reservoir = g[8];
-        const double gm_direct = p[SK_GM_DIRECT];
-        const double rdrf = p[SK_RSV_DRF];
+        const double gm_direct = p[k_gm];
+        const double rdrf = p[k_rsv];
         const double direct = glacier * gm_direct + reservoir * rdrf;
         cc[PC_GLACIER * N + i] = glacier;
         cc[PC_SNOW_STORAGE * N + i] = 1.0 - lake - reservoir;
@@ -293,7 +303,7 @@ void update_derived(shyft_hip_region* h) {
     if (!h->has_params) throw std::runtime_error("region: parameters not set");
     if (h->dt <= 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
     if (h->hbv()) return update_derived_hbv(h);
-    if (h->ptssk()) return update_derived_ptssk(h);
+    if (h->ptssk() || h->pthsk()) return update_derived_ptssk(h);
     const size_t N = h->n;
     const double dt_s = double(h->dt) / 1e6;
     const double dt_in_days = dt_s / 86400.0;
@@ -439,7 +449,8 @@ const char* shyft_hip_last_error(const shyft_hip_region* h) { return h ? h->err.
 int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_region** out) {
     if (!out) return fail(nullptr, "shyft_hip_region_create: out is null");
     *out = nullptr;
-    if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK && stack != SHYFT_HIP_PT_SS_K)
+    if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK && stack != SHYFT_HIP_PT_SS_K &&
+        stack != SHYFT_HIP_PT_HS_K)
         return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
     if (n_cells == 0 || n_cells > (size_t)INT32_MAX) return fail(nullptr, "shyft_hip_region_create: invalid n_cells");
     std::unique_ptr<shyft_hip_region> h(new shyft_hip_region());
@@ -520,6 +531,9 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
                 throw std::runtime_error("HBV_Stack Parameter Accessor: .set size missmatch");
         } else if (h->ptssk()) {
             if (n_per_set != PTSSK_NP) throw std::runtime_error("pt_ss_k parameter accessor: .set size mismatch");
+        } else if (h->pthsk()) {
+            if (n_per_set != PTHSK_NP_REF && n_per_set != PTHSK_NP)
+                throw std::runtime_error("pt_ss_k parameter accessor: .set size missmatch");  // pt_hs_k.h:68 text
         } else if (n_per_set != h->n_ref_params()) {
             throw std::runtime_error("PTGSK Parameter Accessor: .set size missmatch");
         }
@@ -536,18 +550,19 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
         for (size_t k = 0; k < n_sets; ++k) {
             double* q = &h->params[k * width];
             for (size_t j = 0; j < n_per_set; ++j) q[j] = params[k * n_per_set + j];
-            if (h->hbv() && n_per_set == HBV_NP_REF) {
+            const int kd = h->snow_dist_index();  // HK_NB / PH_NB: n_bins, s[HBV_MAX_BINS], intervals[HBV_MAX_BINS]
+            if (kd >= 0 && n_per_set == h->n_ref_params()) {
                 // hbv_snow::parameter() default distribution: s = 1 (normalised mean of ones is exactly 1),
                 // quantiles 0, .25, .5, .75, 1 (hbv_snow.h:29-41)
                 static const double I5[5] = {0.0, 0.25, 0.5, 0.75, 1.0};
-                q[HK_NB] = 5.0;
+                q[kd] = 5.0;
                 for (int b = 0; b < 5; ++b) {
-                    q[HK_S0 + b] = 1.0;
-                    q[HK_I0 + b] = I5[b];
+                    q[kd + 1 + b] = 1.0;
+                    q[kd + 1 + HBV_MAX_BINS + b] = I5[b];
                 }
             }
-            if (h->hbv()) {
-                const double nb = q[HK_NB];
+            if (kd >= 0) {
+                const double nb = q[kd];
                 if (!(nb >= 2.0 && nb <= double(HBV_MAX_BINS)) || nb != double(int(nb)))
                     throw std::runtime_error("hbv_snow: number of snow bins must be in [2, " +
                                              std::to_string(HBV_MAX_BINS) + "]");
@@ -944,7 +959,7 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     size_t b = n_steps > 0 ? size_t(start_step) : 0;
     size_t e = n_steps > 0 ? size_t(start_step + n_steps) : h->T;
     check_window(h, b, e - b, "run_cells");
-    if (h->ptssk()) {
+    if (h->ptssk() || h->pthsk()) {
         ptssk_kargs a;
         a.n_cells = int(h->n);
         a.step0 = int(b);
@@ -968,7 +983,10 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.active = h->active.empty() ? nullptr : h->d_active.p;
         a.err = h->d_err.p;
         hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
-        hip_check(launch_ptssk_run(a, h->stream), "ptssk_run_kernel launch");
+        if (h->pthsk())
+            hip_check(launch_pthsk_run(a, h->stream), "pthsk_run_kernel launch");
+        else
+            hip_check(launch_ptssk_run(a, h->stream), "ptssk_run_kernel launch");
         hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
         return;
     }
@@ -1029,7 +1047,9 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
 }
 
 static void finish_run(shyft_hip_region* h) {
-    hip_check(hipStreamSynchronize(h->stream), h->hbv() ? "hbv_run_kernel" : "ptgsk_run_kernel");
+    hip_check(hipStreamSynchronize(h->stream), h->hbv() ? "hbv_run_kernel"
+                                               : h->ptssk() ? "ptssk_run_kernel"
+                                               : h->pthsk() ? "pthsk_run_kernel" : "ptgsk_run_kernel");
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
     h->last_ms = ms;

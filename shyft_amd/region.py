@@ -12,7 +12,7 @@ import numpy as np
 
 from ._native import check, lib
 
-PT_GS_K, HBV_STACK, PT_SS_K = 1, 2, 3
+PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K = 1, 2, 3, 4
 TEMPERATURE, PRECIPITATION, WIND_SPEED, REL_HUM, RADIATION = range(5)
 FORCING_NAMES = ("temperature", "precipitation", "wind_speed", "rel_hum", "radiation")
 COLLECT_DISCHARGE, COLLECT_DISCHARGE_SNOW, COLLECT_ALL = 0, 1, 2
@@ -30,9 +30,15 @@ SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
 PTSSK_STATE = ("nu", "alpha", "sca", "swe", "free_water", "residual", "num_units", "kirchner_q")
 PTSSK_STATE_SERIES = ("kirchner_discharge", "snow_sca", "snow_swe", "snow_alpha", "snow_nu", "snow_lwc",
                       "snow_residual")
-STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22, PT_SS_K: 21}
-STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE), PT_SS_K: len(PTSSK_STATE)}
-STACK_NSERIES = {PT_GS_K: len(PTGSK_SERIES), HBV_STACK: len(HBV_SERIES), PT_SS_K: len(PTGSK_SERIES)}
+# pt_hs_k (core/pt_hs_k.h:148-172, pt_hs_k_cell_model.h:148-210); response series ids are the pt_gs_k ones
+PTHSK_STATE = (("swe", "sca", "n_bins") + tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) +
+               tuple(f"sw{i}" for i in range(HBV_MAX_BINS)) + ("kirchner_q",))
+PTHSK_STATE_SERIES = (("kirchner_discharge", "snow_sca", "snow_swe") + tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) +
+                      tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
+STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22, PT_SS_K: 21, PT_HS_K: 18}
+STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE), PT_SS_K: len(PTSSK_STATE), PT_HS_K: len(PTHSK_STATE)}
+STACK_NSERIES = {PT_GS_K: len(PTGSK_SERIES), HBV_STACK: len(HBV_SERIES), PT_SS_K: len(PTGSK_SERIES),
+                 PT_HS_K: len(PTGSK_SERIES)}
 
 
 def _ptr(a: np.ndarray | None):

@@ -192,3 +192,30 @@ def default_ptssk_state(n_cells: int, q: float = 1.0) -> np.ndarray:
     s[:, 1] = 40.77
     s[:, 7] = q
     return s
+
+
+def default_pthsk_parameters() -> np.ndarray:
+    """PTHSKParameter() defaults in the reference get/set order (core/pt_hs_k.h:66-88)."""
+    return np.array([
+        -2.439, 0.966, -0.10,            # kirchner c1 c2 c3 (kirchner.h:120-125)
+        1.5,                             # ae.ae_scale_factor
+        0.1, 0.0, 1.0, 0.0, 0.5,         # hs lw tx cx ts cfr (hbv_snow.h:49-53)
+        6.0,                             # gm.dtf
+        1.0,                             # p_corr.scale_factor
+        0.2, 1.26,                       # pt.albedo pt.alpha
+        1.0, 7.0, 0.0,                   # routing velocity alpha beta
+        0.0,                             # gm.direct_response
+        1.0,                             # msp.reservoir_direct_response_fraction
+    ], dtype=np.float64)
+
+
+PTHSK_NS = 3 + 2 * HBV_MAX_BINS + 1  # swe sca n_bins sp[8] sw[8] kirchner.q
+
+
+def default_pthsk_state(n_cells: int, q: float = 1.0, swe: float = 0.0, sca: float = 0.0) -> np.ndarray:
+    """PTHSKState(): hbv_snow::state(swe, sca) undistributed (hbv_snow.h:74-99) with kirchner.q = q."""
+    s = np.zeros((n_cells, PTHSK_NS), dtype=np.float64)
+    s[:, 0] = swe
+    s[:, 1] = sca
+    s[:, -1] = q
+    return s

@@ -122,3 +122,40 @@ def run_ptssk(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0,
         return out
     finally:
         r.close()
+
+
+def run_pthsk(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, snow_dist=None,
+              full=True, collect_state=False):
+    """pt_hs_k region; forcing [5][T][N]; params [n_sets][18]; state [N][20].
+    Returns dict main [2][T][N], full [8][T][N], state [N][20] (+ state_series [19][T+1][N])."""
+    geo11 = np.atleast_2d(geo11)
+    if engine == "oracle":
+        return oracle_lib.pthsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step, n_steps, set_ix,
+                                    snow_dist=snow_dist, full=full, collect_state=collect_state)
+    from shyft_amd.region import HipRegion, PT_HS_K, COLLECT_ALL, COLLECT_DISCHARGE, PTHSK_STATE, PTHSK_STATE_SERIES
+    N = geo11.shape[0]
+    T = forcing.shape[1]
+    p = np.atleast_2d(np.asarray(params, dtype=np.float64))
+    if snow_dist is not None:
+        p = np.concatenate([p, np.atleast_2d(snow_dist)], axis=1)  # the 35-wide C-ABI row
+    r = HipRegion(PT_HS_K, N)
+    try:
+        r.set_geo(geo11)
+        r.set_parameters(p, set_ix)
+        r.set_time_axis(t0_us, dt_us, T)
+        r.set_collection(COLLECT_ALL if full else COLLECT_DISCHARGE, collect_state)
+        r.set_state(np.asarray(state).reshape(N, len(PTHSK_STATE)))
+        for v in range(5):
+            r.set_forcing(v, 0, forcing[v])
+        r.run_cells(0, start_step, n_steps)
+        out = {"state": r.get_state()}
+        ns = 8 if full else 2
+        allser = np.stack([r.get_series(k, 0, T) for k in range(ns)])
+        out["main"] = allser[:2]
+        if full:
+            out["full"] = allser
+        if collect_state:
+            out["state_series"] = np.stack([r.get_state_series(k, 0, T + 1) for k in range(len(PTHSK_STATE_SERIES))])
+        return out
+    finally:
+        r.close()

@@ -82,6 +82,8 @@ def load(variant: str = "detmath"):
     L.oracle_skaugen_sca_rel_red.argtypes = [C.c_uint64, C.c_uint64, _d, _d]
     L.oracle_ptssk_run.restype = C.c_int
     L.oracle_ptssk_run.argtypes = L.oracle_ptgsk_run.argtypes
+    L.oracle_pthsk_run.restype = C.c_int
+    L.oracle_pthsk_run.argtypes = L.oracle_hbv_run.argtypes
     L.oracle_route.restype = C.c_int
     L.oracle_route.argtypes = [C.c_size_t, C.c_size_t, C.c_int64] + [C.c_void_p] * 4 + [C.c_size_t] + \
         [C.c_void_p] * 4 + [C.c_int64] + [C.c_void_p] * 3
@@ -278,3 +280,38 @@ def hbv_snow_state(swe=0.0, sca=0.0, sm=0.0, uz=20.0, lz=10.0):
     v = np.zeros(HBV_FLAT)
     v[:5] = [swe, sca, sm, uz, lz]
     return v
+
+
+PTHSK_FLAT = 3 + 2 * HBV_MAX_BINS + 1   # swe sca n_bins sp[8] sw[8] kirchner.q
+PTHSK_NSC = 3 + 2 * HBV_MAX_BINS        # kirchner_discharge snow_sca snow_swe sp[8] sw[8]
+
+
+def pthsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, snow_dist=None,
+              full=False, collect_state=False, ncore=0, variant="detmath"):
+    """Run the oracle pt_hs_k region. params [n_sets][18]; snow_dist [n_sets][17] or None (default 5 bins);
+    state [N][20]. Returns dict main [2][T][N], full [8][T][N], state_series [19][T+1][N], state [N][20]."""
+    L = load(variant)
+    geo11 = np.ascontiguousarray(geo11, dtype=np.float64)
+    N = geo11.shape[0]
+    params = np.ascontiguousarray(np.atleast_2d(params), dtype=np.float64)
+    dist = None if snow_dist is None else np.ascontiguousarray(np.atleast_2d(snow_dist), dtype=np.float64)
+    st = np.ascontiguousarray(state, dtype=np.float64).reshape(N, PTHSK_FLAT).copy()
+    F = np.ascontiguousarray(forcing, dtype=np.float64)
+    T = F.shape[1]
+    ix = None if set_ix is None else np.ascontiguousarray(set_ix, dtype=np.int32)
+    out_main = np.empty((2, T, N))
+    out_full = np.empty((8, T, N)) if full else None
+    out_state = np.empty((PTHSK_NSC, T + 1, N)) if collect_state else None
+    el = C.c_double(0.0)
+    err = C.create_string_buffer(512)
+    rc = L.oracle_pthsk_run(N, _p(geo11), _p(params), _p(dist), params.shape[0], _p(ix), _p(st), int(t0_us),
+                            int(dt_us), T, int(start_step), int(n_steps), _p(F[0]), _p(F[1]), _p(F[2]), _p(F[3]),
+                            _p(F[4]), _p(out_main), _p(out_full), _p(out_state), int(ncore), C.byref(el), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    r = {"main": out_main, "state": st, "elapsed_s": el.value}
+    if full:
+        r["full"] = out_full
+    if collect_state:
+        r["state_series"] = out_state
+    return r
