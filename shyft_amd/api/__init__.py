@@ -364,6 +364,92 @@ class _FlatState:
         return isinstance(other, type(self)) and np.allclose(self._v, other._v, atol=1e-6)
 
 
+# ---- cell-identified state (api/api_state.h:22-146; api/boostpython/api_state.cpp) -----------------------------------
+CellStateId = _api.CellStateId
+
+
+def byte_vector_to_file(path, byte_vector):
+    """api.byte_vector_to_file: write a serialised state blob to a file."""
+    with open(path, "wb") as f:
+        f.write(bytes(byte_vector))
+
+
+def byte_vector_from_file(path):
+    """api.byte_vector_from_file: read a blob written by byte_vector_to_file."""
+    with open(path, "rb") as f:
+        return f.read()
+
+
+class _StateWithId:
+    """cell_state_with_id<state_t> (api_state.h:62-75): id + state."""
+    _state_t = None
+
+    def __init__(self, id=None, state=None):
+        self.id = id if id is not None else CellStateId()
+        self.state = state if state is not None else self._state_t()
+
+    def __eq__(self, other):  # only id equality (api_state.h:68-70)
+        return isinstance(other, _StateWithId) and self.id == other.id
+
+
+class _StateWithIdVector(_Vector):
+    """vector<cell_state_with_id<state_t>> with the reference's serialisation helpers. The byte layout is this
+    engine's own (host/state_io.hpp), tagged with the method stack; it is not a boost archive."""
+    _item_t = None
+    _state_vector_t = None
+    _stack = 0
+
+    def _pairs(self):
+        return [(x.id, x.state.to_vector()) for x in self]
+
+    @classmethod
+    def _from_pairs(cls, pairs):
+        return cls(cls._item_t(i, cls._item_t._state_t(v)) for i, v in pairs)
+
+    def serialize_to_bytes(self):
+        return _api._serialize_states(self._stack, len(self._item_t._state_t.NAMES), self._pairs())
+
+    @classmethod
+    def deserialize_from_bytes(cls, b):
+        return cls._from_pairs(_api._deserialize_states(bytes(b), cls._stack, len(cls._item_t._state_t.NAMES)))
+
+    def serialize_to_str(self):
+        import base64
+        return base64.b64encode(self.serialize_to_bytes()).decode("ascii")
+
+    @classmethod
+    def deserialize_from_str(cls, s):
+        import base64
+        return cls.deserialize_from_bytes(base64.b64decode(s))
+
+    @property
+    def state_vector(self):
+        return self._state_vector_t(x.state for x in self)
+
+
+def make_state_with_id_types(prefix, state_t, state_vector_t, stack_id):
+    """<prefix>StateWithId, <prefix>StateWithIdVector and the module-level deserialize_from_bytes of a stack."""
+    item = type(prefix + "StateWithId", (_StateWithId,), {"_state_t": state_t})
+    vec = type(prefix + "StateWithIdVector", (_StateWithIdVector,),
+               {"_item_t": item, "_state_vector_t": state_vector_t, "_stack": stack_id})
+    return item, vec, vec.deserialize_from_bytes
+
+
+class _StateIoHandler:
+    """model.state: state_io_handler<cell_t> (api_state.h:99-146)."""
+
+    def __init__(self, model):
+        self._m = model
+
+    def extract_state(self, cids):
+        """the states of the cells (all, or those of the catchment ids `cids`) with their CellStateId"""
+        return self._m._state_with_id_vector_t._from_pairs(self._m._extract_state(list(cids)))
+
+    def apply_state(self, cell_id_state_vector, cids):
+        """apply states by CellStateId (filtered by cids); returns the indexes of states that matched no cell"""
+        return IntVector(self._m._apply_state(list(cell_id_state_vector._pairs()), list(cids)))
+
+
 # ---- cell views (core/cell_model.h:47-160) ---------------------------------------------------------------------------
 FORCING = ("temperature", "precipitation", "wind_speed", "rel_hum", "radiation")
 SERIES_FORCING, SERIES_STATE = 100, 200
@@ -592,6 +678,10 @@ class _ModelMixin:
     @property
     def current_state(self):
         return self.get_states()
+
+    @property
+    def state(self):
+        return _StateIoHandler(self)
 
     @property
     def initial_state(self):

@@ -2,7 +2,8 @@
 shyft/api/hbv_stack/__init__.py) over the MI355X engine."""
 from __future__ import annotations
 
-from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE)
+from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE,
+                make_state_with_id_types)
 
 # get/set order and names (core/hbv_stack.h:82-170), defaults (hbv_soil.h:19-24, hbv_actual_evapotranspiration.h,
 # hbv_tank.h:19-31, hbv_snow.h:49-53, routing.h:76)
@@ -63,7 +64,13 @@ _STATE_SERIES = ("snow_swe", "snow_sca", "soil_moisture", "tank_uz", "tank_lz", 
     tuple(f"sp{i}" for i in range(MAX_BINS)) + tuple(f"sw{i}" for i in range(MAX_BINS))
 
 
+# cell-identified state (api_state.h:62-75) and its serialisation (api/boostpython/api_state.cpp)
+HbvStateWithId, HbvStateWithIdVector, deserialize_from_bytes = make_state_with_id_types(
+    "Hbv", HbvState, HbvStateVector, 2)
+
+
 class _HbvBase(_ModelMixin):
+    _state_with_id_vector_t = HbvStateWithIdVector
     _parameter_t = HbvParameter
     _state_t = HbvState
     _state_vector_t = HbvStateVector

@@ -2,7 +2,8 @@
 shyft/api/pt_gs_k/__init__.py:5-63) over the MI355X engine."""
 from __future__ import annotations
 
-from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE)
+from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE,
+                make_state_with_id_types)
 
 # get/set order and names of pt_gs_k::parameter (core/pt_gs_k.h:77-112, get_name :155-190), defaults of the
 # member structs (kirchner.h:120-125, gamma_snow.h:46-97, priestley_taylor.h, routing.h:76, mstack_param.h)
@@ -50,7 +51,13 @@ _STATE_SERIES = ("kirchner_discharge", "gs_albedo", "gs_lwc", "gs_surface_heat",
                  "gs_acc_melt", "gs_iso_pot_energy", "gs_temp_swe")
 
 
+# cell-identified state (api_state.h:62-75) and its serialisation (api/boostpython/api_state.cpp)
+PTGSKStateWithId, PTGSKStateWithIdVector, deserialize_from_bytes = make_state_with_id_types(
+    "PTGSK", PTGSKState, PTGSKStateVector, 1)
+
+
 class _PTGSKBase(_ModelMixin):
+    _state_with_id_vector_t = PTGSKStateWithIdVector
     _parameter_t = PTGSKParameter
     _state_t = PTGSKState
     _state_vector_t = PTGSKStateVector

@@ -2,7 +2,8 @@
 shyft/api/pt_hs_k/__init__.py) over the MI355X engine."""
 from __future__ import annotations
 
-from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE)
+from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE,
+                make_state_with_id_types)
 
 # get/set order and names (core/pt_hs_k.h:66-143); defaults of the member structs (kirchner.h:120-125,
 # hbv_snow.h:49-53, priestley_taylor.h, glacier_melt.h, routing.h:76, mstack_param.h)
@@ -57,7 +58,13 @@ _STATE_SERIES = (("kirchner_discharge", "snow_sca", "snow_swe") + tuple(f"snow_s
                  tuple(f"snow_sw{i}" for i in range(MAX_BINS)))
 
 
+# cell-identified state (api_state.h:62-75) and its serialisation (api/boostpython/api_state.cpp)
+PTHSKStateWithId, PTHSKStateWithIdVector, deserialize_from_bytes = make_state_with_id_types(
+    "PTHSK", PTHSKState, PTHSKStateVector, 4)
+
+
 class _PTHSKBase(_ModelMixin):
+    _state_with_id_vector_t = PTHSKStateWithIdVector
     _parameter_t = PTHSKParameter
     _state_t = PTHSKState
     _state_vector_t = PTHSKStateVector

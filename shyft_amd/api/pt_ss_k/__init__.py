@@ -2,7 +2,8 @@
 shyft/api/pt_ss_k/__init__.py) over the MI355X engine."""
 from __future__ import annotations
 
-from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE)
+from .. import (_api, _FlatParameter, _FlatState, _ModelMixin, _Statistics, _Vector, SERIES_STATE,
+                make_state_with_id_types)
 
 # get/set order and names (core/pt_ss_k.h:78-150); defaults of the member structs (skaugen.h:89-112,
 # kirchner.h:120-125, priestley_taylor.h, routing.h:76, mstack_param.h)
@@ -37,7 +38,13 @@ _SERIES = ("avg_discharge", "charge_m3s", "snow_sca", "snow_total_stored_water",
 _STATE_SERIES = ("kirchner_discharge", "snow_sca", "snow_swe", "snow_alpha", "snow_nu", "snow_lwc", "snow_residual")
 
 
+# cell-identified state (api_state.h:62-75) and its serialisation (api/boostpython/api_state.cpp)
+PTSSKStateWithId, PTSSKStateWithIdVector, deserialize_from_bytes = make_state_with_id_types(
+    "PTSSK", PTSSKState, PTSSKStateVector, 3)
+
+
 class _PTSSKBase(_ModelMixin):
+    _state_with_id_vector_t = PTSSKStateWithIdVector
     _parameter_t = PTSSKParameter
     _state_t = PTSSKState
     _state_vector_t = PTSSKStateVector

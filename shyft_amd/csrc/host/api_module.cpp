@@ -68,6 +68,8 @@ void bind_model(py::module_& m, const char* name) {
         .def("_get_states", [](const M& x) { return x.current_state(); })
         .def("_set_states", &M::set_states)
         .def("revert_to_initial_state", &M::revert_to_initial_state)
+        .def("_extract_state", &M::extract_state)
+        .def("_apply_state", &M::apply_state)
         .def("adjust_q", &M::adjust_q, py::arg("q_scale"), py::arg("cids"))
         .def("adjust_state_to_target_flow", &M::adjust_state_to_target_flow, py::arg("wanted_flow_m3s"),
              py::arg("cids"), py::arg("start_step") = 0, py::arg("scale_range") = 3.0, py::arg("scale_eps") = 1e-3,
@@ -282,6 +284,30 @@ PYBIND11_MODULE(_api, m) {
              }),
              py::arg("scale_factor") = 1.02, py::arg("max_members") = 20, py::arg("max_distance") = 200000.0)
         .def_readwrite("scale_factor", &idw_precipitation_parameter::scale_factor);
+    // CellStateId (api/api_state.h:34-59; api/boostpython/api_state.cpp)
+    py::class_<cell_state_id>(m, "CellStateId")
+        .def(py::init<>())
+        .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("cid"), py::arg("x"), py::arg("y"), py::arg("area"))
+        .def_readwrite("cid", &cell_state_id::cid)
+        .def_readwrite("x", &cell_state_id::x)
+        .def_readwrite("y", &cell_state_id::y)
+        .def_readwrite("area", &cell_state_id::area)
+        .def("__eq__", &cell_state_id::operator==)
+        .def("__ne__", &cell_state_id::operator!=)
+        .def("__lt__", &cell_state_id::operator<)
+        .def("__hash__", [](const cell_state_id& c) { return py::hash(py::make_tuple(c.cid, c.x, c.y, c.area)); })
+        .def("__repr__", [](const cell_state_id& c) {
+            return "CellStateId(" + std::to_string(c.cid) + ", " + std::to_string(c.x) + ", " + std::to_string(c.y) +
+                   ", " + std::to_string(c.area) + ")";
+        });
+    m.def("_serialize_states", [](int stack, size_t n_fields, const std::vector<state_with_id>& v) {
+        auto b = serialize_states(stack, n_fields, v);
+        return py::bytes(b.data(), b.size());
+    });
+    m.def("_deserialize_states", [](const py::bytes& b, int stack, size_t n_fields) {
+        std::string s = b;
+        return deserialize_states(std::vector<char>(s.begin(), s.end()), stack, n_fields);
+    });
     // BTKParameter (api/boostpython/api_interpolation.cpp:188-200)
     py::class_<btk_parameter>(m, "BTKParameter")
         .def(py::init<>())

@@ -30,6 +30,7 @@
 #include "../../../include/shyft_hip.h"
 #include "optimize.hpp"
 #include "routing.hpp"
+#include "state_io.hpp"
 #include "time_series.hpp"
 
 namespace shyft_hip::host {
@@ -436,6 +437,16 @@ class region_model {
         if (states.size() != size()) throw std::runtime_error("Length of the state vector must equal number of cells");
         put_states(states);
         if (initial_state.size() != states.size()) initial_state = states;
+    }
+    // state_io_handler (api/api_state.h:99-146): model.state.extract_state / apply_state
+    std::vector<state_with_id> extract_state(const std::vector<int64_t>& cids) const {
+        return shyft_hip::host::extract_state(geo_, current_state(), cids);
+    }
+    std::vector<int64_t> apply_state(const std::vector<state_with_id>& s, const std::vector<int64_t>& cids) {
+        auto st = current_state();
+        auto missing = shyft_hip::host::apply_state(geo_, st, s, cids);
+        put_states(st);  // cell.state = ... (initial_state is not touched, api_state.h:139)
+        return missing;
     }
     void revert_to_initial_state() {
         if (initial_state.empty()) throw std::runtime_error("Initial state not yet established or set");

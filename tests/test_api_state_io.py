@@ -1,0 +1,115 @@
+"""Cell-identified state: model.state.extract_state / apply_state, <Stack>StateWithIdVector serialisation
+(api/api_state.h:22-146; shyft/tests/api/test_region_model_stacks.py:71-78 verify_state_handler and :557-627
+test_state_with_id_handler).
+
+The byte / string forms are this engine's own layout (host/state_io.hpp), not boost archives: they round-trip
+here and are refused by another method stack. CPU tests cover the format; GPU tests the model handler."""
+import os
+import tempfile
+
+import pytest
+
+
+def test_state_blob_roundtrip_and_stack_tag():
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k, hbv_stack
+    v = pt_gs_k.PTGSKStateWithIdVector()
+    for i in range(5):
+        s = pt_gs_k.PTGSKState()
+        s.kirchner.q = 100.0 + i
+        v.append(pt_gs_k.PTGSKStateWithId(api.CellStateId(1 + i % 2, 500 + 1000 * i, 500, 1000000), s))
+    b = v.serialize_to_bytes()
+    w = pt_gs_k.deserialize_from_bytes(b)
+    assert len(w) == 5
+    for a, c in zip(w, v):
+        assert a.id == c.id and a.state.kirchner.q == c.state.kirchner.q
+    x = pt_gs_k.PTGSKStateWithIdVector.deserialize_from_str(v.serialize_to_str())
+    assert [a.state.to_vector() for a in x] == [a.state.to_vector() for a in v]
+    with pytest.raises(RuntimeError, match="another method stack"):
+        hbv_stack.deserialize_from_bytes(b)
+    with pytest.raises(RuntimeError, match="truncated"):
+        pt_gs_k.deserialize_from_bytes(b[:-3])
+    with tempfile.TemporaryDirectory() as d:
+        f = os.path.join(d, "s.bin")
+        api.byte_vector_to_file(f, b)
+        assert api.byte_vector_from_file(f) == b
+    sv = v.state_vector
+    assert len(sv) == 5 and sv[2].kirchner.q == 102.0
+    assert api.CellStateId(1, 2, 3, 4) < api.CellStateId(1, 2, 4, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stack", ["pt_gs_k", "hbv_stack", "pt_ss_k", "pt_hs_k"])
+def test_verify_state_handler(stack):
+    """verify_state_handler (test_region_model_stacks.py:71-78) for every stack's model."""
+    import importlib
+    from shyft_amd import api
+    from tests.test_api_region_model import build_model
+    m = importlib.import_module(f"shyft_amd.api.{stack}")
+    pre = {"pt_gs_k": "PTGSK", "hbv_stack": "Hbv", "pt_ss_k": "PTSSK", "pt_hs_k": "PTHSK"}[stack]
+    model = build_model(getattr(m, pre + "Model"), getattr(m, pre + "Parameter"), 20)
+    cids = api.IntVector()
+    states = model.state.extract_state(cids)
+    assert len(states) == model.size()
+    states2 = states.__class__.deserialize_from_str(str(states.serialize_to_str()))
+    assert len(states2) == len(states)
+    assert len(model.state.apply_state(states, cids)) == 0
+
+
+@pytest.mark.gpu
+def test_state_with_id_handler():
+    """test_state_with_id_handler (test_region_model_stacks.py:557-627)."""
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k
+    from tests.test_api_region_model import build_model
+    model = build_model(pt_gs_k.PTGSKModel, pt_gs_k.PTGSKParameter, 20, 2)
+    cids_unspecified = api.IntVector()
+    cids_1 = api.IntVector([1])
+    cids_2 = api.IntVector([2])
+    model_state_12 = model.state.extract_state(cids_unspecified)
+    model_state_1 = model.state.extract_state(cids_1)
+    model_state_2 = model.state.extract_state(cids_2)
+    assert len(model_state_1) + len(model_state_2) == len(model_state_12)
+    ms2 = pt_gs_k.PTGSKStateWithIdVector.deserialize_from_str(model_state_2.serialize_to_str())
+    assert len(ms2) == len(model_state_2)
+    for a, b in zip(ms2, model_state_2):
+        assert a.id == b.id
+        assert a.state.kirchner.q == pytest.approx(b.state.kirchner.q)
+    assert len(model_state_1) > 0 and len(model_state_2) > 0
+    assert all(x.id.cid == 1 for x in model_state_1)
+    assert all(x.id.cid == 2 for x in model_state_2)
+    for i in range(len(model_state_12)):
+        model_state_12[i].state.kirchner.q = 100 + i
+    model.state.apply_state(model_state_12, cids_unspecified)
+    ms_12 = model.state.extract_state(cids_unspecified)
+    for i in range(len(ms_12)):
+        assert ms_12[i].state.kirchner.q == pytest.approx(100 + i)
+    for i in range(len(model_state_2)):
+        model_state_2[i].state.kirchner.q = 200 + i
+    unapplied = model.state.apply_state(model_state_2, cids_2)
+    assert len(unapplied) == 0
+    ms_12 = model.state.extract_state(cids_unspecified)
+    for i in range(len(ms_12)):
+        if ms_12[i].id.cid == 1:
+            assert ms_12[i].state.kirchner.q == pytest.approx(100 + i)
+    ms_2 = model.state.extract_state(cids_2)
+    for i in range(len(ms_2)):
+        assert ms_2[i].state.kirchner.q == pytest.approx(200 + i)
+    b = ms_2.serialize_to_bytes()
+    with tempfile.TemporaryDirectory() as d:
+        f = os.path.join(d, "pt_gs_k_state_test.bin")
+        api.byte_vector_to_file(f, b)
+        b = api.byte_vector_from_file(f)
+    ms_2x = pt_gs_k.deserialize_from_bytes(b)
+    for i in range(len(ms_2x)):
+        assert ms_2x[i].state.kirchner.q == pytest.approx(200 + i)
+    sv_2 = ms_2.state_vector
+    assert len(sv_2) == len(ms_2)
+    for s, sid in zip(sv_2, ms_2):
+        assert s.kirchner.q == pytest.approx(sid.state.kirchner.q)
+    model.state.apply_state(ms_2, cids_unspecified)
+    model.initial_state = model.current_state
+    # a state for a cell that does not exist is reported, not applied
+    extra = pt_gs_k.PTGSKStateWithIdVector(list(ms_2))
+    extra.append(pt_gs_k.PTGSKStateWithId(api.CellStateId(2, 123, 456, 1000000), pt_gs_k.PTGSKState()))
+    assert list(model.state.apply_state(extra, cids_unspecified)) == [len(ms_2)]
