@@ -294,10 +294,10 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
-def pmc_traffic(stack, cells, chunk):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (profiles/r01/<stack>_pmc.json, FETCH_SIZE + WRITE_SIZE, tools/gpu_profile.sh) when they were taken on
-    this exact workload; None otherwise. PMC counters cannot be read from inside this process."""
+def pmc_summary(stack, cells, chunk):
+    """The committed rocprofv3 PMC summary of the dominant kernel (profiles/r01/<stack>_pmc.json, written by
+    tools/gpu_profile.sh + tools/pmc_summary.py) when it was taken on this exact workload; None otherwise. PMC
+    counters cannot be read from inside this process."""
     path = os.path.join(ROOT, "profiles", "r01", f"{stack.replace('_', '')}_pmc.json")
     try:
         d = json.load(open(path))
@@ -305,7 +305,7 @@ def pmc_traffic(stack, cells, chunk):
         return None
     if d.get("cells") != cells or d.get("chunk") != chunk:
         return None
-    return d["traffic_bytes_per_launch"]
+    return d
 
 
 def _cpu_model():
@@ -358,7 +358,8 @@ def main():
     value = total_cell_steps / wall
     bytes_per_launch = cells * chunk * (read_b + write_b) + cells * state_b
     achieved = bytes_per_launch / (avg_kernel_ms * 1e-3)
-    traffic_b = pmc_traffic(a.stack, cells, chunk)
+    pmc = pmc_summary(a.stack, cells, chunk)
+    traffic_b = None if pmc is None else pmc["traffic_bytes_per_launch"]
     out = {
         "metric": METRIC if a.stack == "pt_gs_k" else METRIC.replace("pt_gs_k", a.stack),
         "value": value,
@@ -396,8 +397,8 @@ def main():
             "frac": achieved / HBM_PEAK_BPS,
             "traffic": None if traffic_b is None else traffic_b / (avg_kernel_ms * 1e-3) / 1e9,
             "traffic_bytes_per_launch": traffic_b,
-            "traffic_source": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch (profiles/r01/*_pmc.json), over this "
-                              "run's average launch duration, GB/s like achieved",
+            "traffic_source": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch, mean over the 12 chunks of a year "
+                              "(profiles/r01/*_pmc.json), over this run's average launch duration, GB/s like achieved",
             "kernel": kernel_name,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "note": f"{read_b + write_b} B/cell-step ({read_b} B forcing read + {write_b} B discharge/charge write) + "
@@ -417,6 +418,19 @@ def main():
                          "write_GBps": cells * chunk * 8 / (ms * 1e-3) / 1e9,
                          "note": "2 * cells * (stations + 3) * chunk flops per call over its wall time "
                                  "(host part included)"},
+        }
+    if pmc is not None and "launches" in pmc and "SQ_ACTIVE_INST_VALU" in pmc["launches"][0]:
+        # the bound that does apply: fp64 VALU issue. SQ_ACTIVE_INST_VALU (quad-cycles of VALU issue summed over
+        # waves, mean per launch over a year of chunks) over this run's kernel time on 1024 SIMDs at 2.4 GHz
+        act = float(np.mean([l["SQ_ACTIVE_INST_VALU"] for l in pmc["launches"]]))
+        ins = float(np.mean([l["SQ_INSTS_VALU"] for l in pmc["launches"]]))
+        out["valu"] = {
+            "busy": act * 4.0 / (1024 * 2.4e9 * avg_kernel_ms * 1e-3),
+            "wave_instr_per_launch": ins,
+            "lane_instr_per_cell_step": ins * 64.0 / (cells * chunk),
+            "by_chunk_busy": [round(l["valu_busy"], 3) for l in pmc["launches"]],
+            "source": "rocprofv3 SQ pass (profiles/r01/*_pmc.json); busy = SQ_ACTIVE_INST_VALU*4 / (1024 SIMDs x "
+                      "2.4 GHz x this run's mean kernel time); by_chunk_busy uses each PMC launch's own duration",
         }
     if router is not None:
         o = router.out[2]

@@ -16,8 +16,8 @@ run() {  # name, extra rocprofv3 args..., then bench args after --
     echo "prof $name ok"
 }
 BARGS="--steps 12 --warmup 1" run trace --kernel-trace --stats
-BARGS="--steps 2 --warmup 0" run fetch --kernel-trace --pmc FETCH_SIZE
-BARGS="--steps 2 --warmup 0" run write --kernel-trace --pmc WRITE_SIZE
-BARGS="--steps 2 --warmup 0" run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
+BARGS="--steps 12 --warmup 0" run fetch --kernel-trace --pmc FETCH_SIZE
+BARGS="--steps 12 --warmup 0" run write --kernel-trace --pmc WRITE_SIZE
+BARGS="--steps 12 --warmup 0" run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
 cd $R
 find gpurun_out -path "*prof_*" -name "*.csv" | sort
