@@ -52,6 +52,7 @@ STACKS = {
     "hbv_stack": (32, 16, 2 * 22 * 8, "hbv_run_kernel"),     # wind not read (hbv_stack.h:295-301); 22 state
     "pt_ss_k": (40, 16, 2 * 8 * 8, "ptssk_run_kernel"),      # T P WS RH RAD in (WS unused by skaugen); 8 state
     "pt_hs_k": (40, 16, 2 * 20 * 8, "pthsk_run_kernel"),     # T P WS RH RAD in; 20 state (hbv_snow bins + q)
+    "pt_hps_k": (40, 16, 2 * 37 * 8, "pthpsk_run_kernel"),   # T P WS RH RAD in; 37 state (hps bins + q)
 }
 
 
@@ -62,7 +63,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=0,
                     help="cells per GPU (default 1,048,576 for pt_gs_k, 524,288 for hbv_stack)")
-    ap.add_argument("--stack", choices=("pt_gs_k", "hbv_stack", "pt_ss_k", "pt_hs_k"), default="pt_gs_k")
+    ap.add_argument("--stack", choices=tuple(STACKS), default="pt_gs_k")
     ap.add_argument("--routing", action="store_true",
                     help="configs[4]: route avg_discharge through the synthetic river network (routing::uhg): "
                          "per chunk the (river, UHG)-group sums are formed on each GPU and all-gathered, after the "
@@ -166,13 +167,15 @@ def stack_defaults(stack, cells):
         return synthetic.default_ptssk_parameters(), synthetic.default_ptssk_state(cells)
     if stack == "pt_hs_k":
         return synthetic.default_pthsk_parameters(), synthetic.default_pthsk_state(cells)
+    if stack == "pt_hps_k":
+        return synthetic.default_pthpsk_parameters(), synthetic.default_pthpsk_state(cells)
     return synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(cells)
 
 
 def build_region(stack, cells, world, rank, local, chunk, n_steps_axis):
     from shyft_amd import synthetic
-    from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K, COLLECT_DISCHARGE
-    sid = {"pt_gs_k": PT_GS_K, "hbv_stack": HBV_STACK, "pt_ss_k": PT_SS_K, "pt_hs_k": PT_HS_K}[stack]
+    from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K, PT_HPS_K, COLLECT_DISCHARGE
+    sid = {"pt_gs_k": PT_GS_K, "hbv_stack": HBV_STACK, "pt_ss_k": PT_SS_K, "pt_hs_k": PT_HS_K, "pt_hps_k": PT_HPS_K}[stack]
     r = HipRegion(sid, cells, device=local)
     r.set_geo(synthetic.geo11(cells, n_catchments=100 * world, cell_offset=rank * cells, n_total=world * cells))
     r.set_parameters(stack_defaults(stack, 1)[0])
@@ -263,8 +266,8 @@ def cpu_baseline(stack, n_cells, threads):
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K
     from tests import oracle_lib
-    run = {"hbv_stack": oracle_lib.hbv_run, "pt_ss_k": oracle_lib.ptssk_run,
-           "pt_hs_k": oracle_lib.pthsk_run}.get(stack, oracle_lib.ptgsk_run)
+    run = {"hbv_stack": oracle_lib.hbv_run, "pt_ss_k": oracle_lib.ptssk_run, "pt_hs_k": oracle_lib.pthsk_run,
+           "pt_hps_k": oracle_lib.pthpsk_run}.get(stack, oracle_lib.ptgsk_run)
     # forcing of the sample cells: identical bits from the device generator (tests/test_capi.py pins equality)
     g = HipRegion(PT_GS_K, n_cells, device=0)
     g.set_geo(synthetic.geo11(n_cells, n_total=1 << 20))
@@ -381,7 +384,7 @@ def main():
                          else f"{a.stack} ") +
                         f"region_model::run_cells, {cells} cells/GPU x {chunk * a.steps} hourly steps "
                         f"({a.steps} chunks of {chunk}), discharge_collector, default "
-                        f"{dict(hbv_stack='HbvParameter', pt_ss_k='PTSSKParameter', pt_hs_k='PTHSKParameter').get(a.stack, 'PTGSKParameter')}",
+                        f"{dict(hbv_stack='HbvParameter', pt_ss_k='PTSSKParameter', pt_hs_k='PTHSKParameter', pt_hps_k='PTHPSKParameter').get(a.stack, 'PTGSKParameter')}",
             "cells_per_gpu": cells,
             "total_cells": world * cells,
             "steps_per_chunk": chunk,

@@ -31,8 +31,10 @@ extern "C" {
 
 typedef struct shyft_hip_region shyft_hip_region;
 
-/* method stacks (core/pt_gs_k.h, core/hbv_stack.h, core/pt_ss_k.h, core/pt_hs_k.h) */
-enum shyft_hip_stack { SHYFT_HIP_PT_GS_K = 1, SHYFT_HIP_HBV_STACK = 2, SHYFT_HIP_PT_SS_K = 3, SHYFT_HIP_PT_HS_K = 4 };
+/* method stacks (core/pt_gs_k.h, core/hbv_stack.h, core/pt_ss_k.h, core/pt_hs_k.h, core/pt_hps_k.h) */
+enum shyft_hip_stack {
+    SHYFT_HIP_PT_GS_K = 1, SHYFT_HIP_HBV_STACK = 2, SHYFT_HIP_PT_SS_K = 3, SHYFT_HIP_PT_HS_K = 4, SHYFT_HIP_PT_HPS_K = 5
+};
 
 /* forcing variables, the cell env_ts of core/cell_model.h:47-81 */
 enum shyft_hip_forcing {
@@ -75,8 +77,9 @@ int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* r
 
 /* Parameters: n_sets rows of the stack's calibration vector in the reference's
  * get/set order (pt_gs_k: 31 values, core/pt_gs_k.h:77-112; hbv_stack 22, hbv_stack.h:82-109;
- * pt_ss_k 21, pt_ss_k.h:78-101; pt_hs_k 18, pt_hs_k.h:66-88). hbv_stack and pt_hs_k rows may carry
- * 17 more values, the hbv_snow distribution: n_bins (2..8), s[8], intervals[8]; set_ix[n_cells]
+ * pt_ss_k 21, pt_ss_k.h:78-101; pt_hs_k 18, pt_hs_k.h:66-88; pt_hps_k 24, pt_hps_k.h:64-90). hbv_stack and
+ * pt_hs_k rows may carry 17 more values, the hbv_snow distribution: n_bins (2..8), s[8], intervals[8]; pt_hps_k
+ * rows may carry 18 more: gm.direct_response, then that distribution; set_ix[n_cells]
  * selects the row of each cell (region parameter + catchment overrides,
  * region_model.h:287-319). set_ix == NULL means row 0 for every cell. */
 int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n_sets, size_t n_per_set,
@@ -104,7 +107,8 @@ int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, siz
 /* State, n_cells x n_fields (pt_gs_k: 9 = gs albedo lwc surface_heat alpha sdc_melt_mean acc_melt
  * iso_pot_energy temp_swe, kirchner q; hbv_stack: 22 = swe sca sm uz lz n_bins sp[8] sw[8];
  * pt_ss_k: 8 = nu alpha sca swe free_water residual num_units q; pt_hs_k: 20 = swe sca n_bins sp[8]
- * sw[8] q). get/set_states (region_model.h:784-805). */
+ * sw[8] q; pt_hps_k: 37 = swe sca surface_heat n_bins sp[8] sw[8] albedo[8] iso_pot_energy[8] q).
+ * get/set_states (region_model.h:784-805). */
 int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_fields);
 int shyft_hip_get_state(const shyft_hip_region* h, double* state, size_t n_fields);
 

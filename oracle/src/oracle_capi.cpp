@@ -468,6 +468,106 @@ int oracle_pthsk_run(size_t n_cells, const double* geo11, const double* params, 
     return 0;
 }
 
+// ---- hbv_physical_snow / pt_hps_k ----
+// One hbv_physical_snow::calculator::step (hbv_physical_snow.h:291-553) on a flat hps state
+// st36 = swe sca surface_heat n_bins sp[8] sw[8] albedo[8] iso_pot_energy[8]; p12 = tx lw cfr wind_scale wind_const
+// surface_magnitude max_albedo min_albedo fast_decay slow_decay snowfall_reset_depth calculate_iso_pot_energy;
+// dist17 = n_bins s[8] intervals[8] (normalised by the caller). distribute: 0 none, 1 force, 2 only on a size mismatch.
+// resp = outflow sca storage. Returns 1 and the message on a throw.
+int oracle_hps_step(double* st36, double* resp, const double* p12, const double* dist17, int distribute, int64_t dt_us,
+                    double T, double rad, double prec_mm_h, double wind_speed, double rel_hum, char* err, size_t errlen) {
+    hbv_physical_snow::parameter p;
+    const size_t nb = size_t(dist17[0]);
+    p.s.assign(dist17 + 1, dist17 + 1 + nb);
+    p.intervals.assign(dist17 + 1 + pt_hps_k::MB, dist17 + 1 + pt_hps_k::MB + nb);
+    p.tx = p12[0]; p.lw = p12[1]; p.cfr = p12[2]; p.wind_scale = p12[3]; p.wind_const = p12[4];
+    p.surface_magnitude = p12[5]; p.max_albedo = p12[6]; p.min_albedo = p12[7]; p.fast_albedo_decay_rate = p12[8];
+    p.slow_albedo_decay_rate = p12[9]; p.snowfall_reset_depth = p12[10]; p.calculate_iso_pot_energy = p12[11] != 0.0;
+    pt_hps_k::state s;
+    std::vector<double> flat(pt_hps_k::FLAT, 0.0);
+    std::copy(st36, st36 + pt_hps_k::FLAT - 1, flat.begin());
+    s.set(flat.data());
+    try {
+        if (distribute) s.hps.distribute(p, distribute == 1);
+        hbv_physical_snow::calculator c(p);
+        hbv_physical_snow::response r;
+        c.step(s.hps, r, dt_us, T, rad, prec_mm_h, wind_speed, rel_hum);
+        resp[0] = r.outflow; resp[1] = r.sca; resp[2] = r.storage;
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    s.get(flat.data());
+    std::copy(flat.begin(), flat.end() - 1, st36);
+    return 0;
+}
+
+// Run the pt_hps_k region model on the CPU with the reference scheduler.
+//  params : n_sets x 24 (pt_hps_k.h:64-90 order); gm_direct : n_sets or null (glacier_melt::parameter default 0);
+//  snow_dist : n_sets x 17 or null (default 5 bins); state : n_cells x 37 in/out (pt_hps_k::FLAT order)
+//  out_main : [2][T][N]; out_full : [8][T][N]; out_state : [36][T+1][N]
+int oracle_pthpsk_run(size_t n_cells, const double* geo11, const double* params, const double* gm_direct,
+                      const double* snow_dist, size_t n_sets, const int32_t* set_ix, double* state, int64_t t0_us,
+                      int64_t dt_us, size_t T, int start_step, int n_steps, const double* temp, const double* prec,
+                      const double* ws, const double* rh, const double* rad, double* out_main, double* out_full,
+                      double* out_state, int ncore, double* elapsed_s, char* err, size_t errlen) {
+    try {
+        pthpsk_region rm;
+        rm.time_axis = fixed_dt(t0_us, dt_us, T);
+        rm.params.resize(n_sets);
+        for (size_t k = 0; k < n_sets; ++k) {
+            rm.params[k].set(params + k * pt_hps_k::parameter::size());
+            if (gm_direct) rm.params[k].gm.direct_response = gm_direct[k];
+            if (snow_dist) {
+                const double* d = snow_dist + k * 17;
+                const size_t nb = size_t(d[0]);
+                rm.params[k].hps.s.assign(d + 1, d + 1 + nb);
+                rm.params[k].hps.intervals.assign(d + 1 + pt_hps_k::MB, d + 1 + pt_hps_k::MB + nb);
+            }
+        }
+        rm.cells.resize(n_cells);
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.geo = geo_cell_data::from_raw(geo11 + i * 11);
+            int32_t k = set_ix ? set_ix[i] : 0;
+            if (k < 0 || size_t(k) >= n_sets) return fail(err, errlen, "oracle_pthpsk_run: parameter set index out of range");
+            c.parameter = &rm.params[k];
+            c.state.set(state + i * pt_hps_k::FLAT);
+            c.temp.resize(T); c.prec.resize(T); c.ws.resize(T); c.rh.resize(T); c.rad.resize(T);
+            for (size_t t = 0; t < T; ++t) {
+                c.temp[t] = temp[t * n_cells + i];
+                c.prec[t] = prec[t * n_cells + i];
+                c.ws[t] = ws[t * n_cells + i];
+                c.rh[t] = rh[t * n_cells + i];
+                c.rad[t] = rad[t * n_cells + i];
+            }
+            c.col.full = out_full != nullptr;
+            c.col.collect_state = out_state != nullptr;
+        }
+        auto t_begin = std::chrono::steady_clock::now();
+        rm.run_cells(size_t(ncore < 0 ? 0 : ncore), start_step, n_steps);
+        auto t_end = std::chrono::steady_clock::now();
+        if (elapsed_s) *elapsed_s = std::chrono::duration<double>(t_end - t_begin).count();
+        for (size_t i = 0; i < n_cells; ++i) {
+            auto& c = rm.cells[i];
+            c.state.get(state + i * pt_hps_k::FLAT);
+            for (size_t t = 0; t < T; ++t) {
+                if (out_main) {
+                    out_main[t * n_cells + i] = c.col.rc[pt_hps_k::AVG_DISCHARGE][t];
+                    out_main[(T + t) * n_cells + i] = c.col.rc[pt_hps_k::CHARGE_M3S][t];
+                }
+                if (out_full)
+                    for (int k = 0; k < pt_hps_k::N_ALL; ++k) out_full[(size_t(k) * T + t) * n_cells + i] = c.col.rc[k][t];
+            }
+            if (out_state)
+                for (size_t k = 0; k < pt_hps_k::N_SC; ++k)
+                    for (size_t t = 0; t <= T; ++t) out_state[(k * (T + 1) + t) * n_cells + i] = c.col.sc[k][t];
+        }
+    } catch (const std::exception& e) {
+        return fail(err, errlen, e.what());
+    }
+    return 0;
+}
+
 }  // extern "C"
 
 // routing::model query (core/routing.h:347-387) for river `query`: local, upstream, output [T].

@@ -15,6 +15,7 @@
 #include "ptgsk.hpp"
 #include "ptssk.hpp"
 #include "pthsk.hpp"
+#include "pthpsk.hpp"
 
 namespace oracle {
 
@@ -77,6 +78,21 @@ struct pthsk_cell {
         col.initialize(ta.size(), start_step, n_steps, geo.area);
         pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
         pt_hs_k::run_pt_hs_k(geo, *parameter, ta, start_step, n_steps, fv, state, col);
+    }
+};
+
+// pt_hps_k cell (pt_hps_k_cell_model.h:236-294)
+struct pthpsk_cell {
+    geo_cell_data geo;
+    const pt_hps_k::parameter* parameter = nullptr;
+    pt_hps_k::state state;
+    std::vector<double> temp, prec, ws, rh, rad;
+    pt_hps_k::collectors col;
+    void run(const fixed_dt& ta, int start_step, int n_steps) {
+        if (parameter == nullptr) throw std::runtime_error("pt_hps_k::run with null parameter attempted");
+        col.initialize(ta.size(), start_step, n_steps, geo.area);
+        pt_gs_k::forcing_view fv{temp.data(), prec.data(), ws.data(), rh.data(), rad.data(), 1};
+        pt_hps_k::run_pt_hps_k(geo, *parameter, ta, start_step, n_steps, fv, state, col);
     }
 };
 
@@ -144,5 +160,6 @@ using ptgsk_region = region_of<ptgsk_cell, pt_gs_k::parameter>;
 using hbv_region = region_of<hbv_cell, hbv_stack::parameter>;
 using ptssk_region = region_of<ptssk_cell, pt_ss_k::parameter>;
 using pthsk_region = region_of<pthsk_cell, pt_hs_k::parameter>;
+using pthpsk_region = region_of<pthpsk_cell, pt_hps_k::parameter>;
 
 }  // namespace oracle

@@ -431,6 +431,7 @@ PYBIND11_MODULE(_api, m) {
     bind_model<hbv_stack_stack>(m, "_HbvRegionModel");
     bind_model<pt_ss_k_stack>(m, "_PTSSKRegionModel");
     bind_model<pt_hs_k_stack>(m, "_PTHSKRegionModel");
+    bind_model<pt_hps_k_stack>(m, "_PTHPSKRegionModel");
 
     py::enum_<target_spec_calc_type>(m, "target_spec_calc_type")
         .value("NASH_SUTCLIFFE", NASH_SUTCLIFFE)
@@ -504,6 +505,7 @@ PYBIND11_MODULE(_api, m) {
     bind_optimizer<hbv_stack_stack>(m, "_HbvOptimizer");
     bind_optimizer<pt_ss_k_stack>(m, "_PTSSKOptimizer");
     bind_optimizer<pt_hs_k_stack>(m, "_PTHSKOptimizer");
+    bind_optimizer<pt_hps_k_stack>(m, "_PTHPSKOptimizer");
 
     py::register_exception_translator([](std::exception_ptr p) {
         try {

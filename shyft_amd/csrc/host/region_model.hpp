@@ -210,6 +210,18 @@ struct pt_hs_k_stack {
     static constexpr const char* param_error = "pt_ss_k parameter accessor: .set size missmatch";  // pt_hs_k.h:68
 };
 
+struct pt_hps_k_stack {
+    static constexpr int id = SHYFT_HIP_PT_HPS_K;
+    static constexpr size_t n_param = 24;   // core/pt_hps_k.h:62 (+ gm.direct_response + 17 distribution values)
+    static constexpr size_t n_state = 37;   // swe sca surface_heat n_bins sp[8] sw[8] albedo[8] iso_pot_energy[8] q
+    static constexpr size_t n_full_series = 8;
+    static constexpr int k_ae_scale = 3;
+    static constexpr int k_routing = 20;
+    static constexpr int state_q = 36;
+    static constexpr double q_min = 0.0;
+    static constexpr const char* param_error = "pt_ss_k parameter accessor: .set size missmatch";  // pt_hps_k.h:70
+};
+
 // ---- region_model ------------------------------------------------------------------------------------------------
 // result of adjust_state_to_target_flow (core/model_state_tuning.h:12-17)
 struct q_adjust_result {
@@ -278,6 +290,12 @@ class region_model {
             return {0.4, 0.1, 30000.0, 1.26, 0.0, 0.0, 0.0, 0.0, 0.1};
         if (Stack::id == SHYFT_HIP_PT_SS_K)  // skaugen::state() (skaugen.h:122-124) + kirchner::state()
             return {4.077, 40.77, 0.0, 0.0, 0.0, 0.0, 0.0, 0.1};
+        if (Stack::id == SHYFT_HIP_PT_HPS_K) {  // hbv_physical_snow::state() (hbv_physical_snow.h:135-146) + kirchner
+            state_t s(Stack::n_state, 0.0);
+            s[2] = 30000.0;
+            s[Stack::state_q] = 0.1;
+            return s;
+        }
         if (Stack::id == SHYFT_HIP_PT_HS_K) {  // hbv_snow::state() undistributed (hbv_snow.h:74-99) + kirchner::state()
             state_t s(Stack::n_state, 0.0);
             s[Stack::state_q] = 0.1;
@@ -787,7 +805,9 @@ class region_model {
 
     void check_param(const parameter_t& p) const {
         const bool has_snow_dist = Stack::id == SHYFT_HIP_HBV_STACK || Stack::id == SHYFT_HIP_PT_HS_K;
-        if (p.size() != Stack::n_param && !(has_snow_dist && p.size() == Stack::n_param + 17))
+        const bool hps = Stack::id == SHYFT_HIP_PT_HPS_K;  // + gm.direct_response + distribution
+        if (p.size() != Stack::n_param && !(has_snow_dist && p.size() == Stack::n_param + 17) &&
+            !(hps && p.size() == Stack::n_param + 18))
             throw std::runtime_error(Stack::param_error);
     }
 

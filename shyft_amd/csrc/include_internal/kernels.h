@@ -57,6 +57,7 @@ struct ptssk_kargs {
     double step_in_days;     // to_seconds(dt)/86400 (skaugen.h:160)
     double dt_hours;         // to_seconds(dt)/3600 (skaugen.h:161)
     double t1_hours;         // kirchner integration end: to_seconds(dt)/to_seconds(1h)
+    double dt_us;            // dt in microseconds (exact integer value)
     const double* params;    // [n_sets][PTSSK_NP]
     const int32_t* set_ix;   // [N]
     const double* cellc;     // [PTGSK_NC][N]
@@ -76,6 +77,11 @@ hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream);
 // state_series [PTHSK_NSC][win_len+1][N]
 using pthsk_kargs = ptssk_kargs;
 hipError_t launch_pthsk_run(const pthsk_kargs& a, hipStream_t stream);
+
+// pt_hps_k (kernels/pthpsk.hip): same arguments; params [n_sets][PTHPSK_NP], state [PTHPSK_NS][N],
+// state_series [PTHPSK_NSC][win_len+1][N]
+using pthpsk_kargs = ptssk_kargs;
+hipError_t launch_pthpsk_run(const pthpsk_kargs& a, hipStream_t stream);
 
 // routing (kernels/routing.hip): river aggregation of (river, UHG) group discharge sums
 struct routing_args {

@@ -120,6 +120,31 @@ enum pthsk_state_series_index {
 };
 // per-cell constants: the pt_gs_k PC_* rows (pt_hs_k.h:233-242 are the same expressions); response series: PR_*
 
+// ------------------------------------------------------------------ pt_hps_k
+// parameter row: the 24 reference values in get/set order (core/pt_hps_k.h:64-90), gm.direct_response (not a
+// calibration value there, glacier_melt::parameter default 0), then the hbv_physical_snow distribution
+// (n_bins, s[HBV_MAX_BINS], intervals[HBV_MAX_BINS], hbv_physical_snow.h:43-44)
+enum pthpsk_param_index {
+    PP_C1 = 0, PP_C2, PP_C3, PP_AE_SCALE, PP_LW, PP_TX, PP_CFR, PP_WIND_SCALE, PP_WIND_CONST, PP_SURFACE_MAGNITUDE,
+    PP_MAX_ALBEDO, PP_MIN_ALBEDO, PP_FAST_DECAY_RATE, PP_SLOW_DECAY_RATE, PP_SNOWFALL_RESET_DEPTH, PP_ISO, PP_DTF,
+    PP_PCORR, PP_PT_ALBEDO, PP_PT_ALPHA, PP_R_VELOCITY, PP_R_ALPHA, PP_R_BETA, PP_RSV_DRF,
+    PP_GM_DIRECT, PP_NB, PP_S0, PP_I0 = PP_S0 + HBV_MAX_BINS, PTHPSK_NP = PP_I0 + HBV_MAX_BINS
+};
+#define PTHPSK_NP_REF 24
+
+// pt_hps_k state (pt_hps_k.h:163-185; hbv_physical_snow.h:135-190): swe sca surface_heat, the number of
+// distributed bins, the bins sp / sw / albedo / iso_pot_energy, kirchner q
+enum pthpsk_state_index {
+    PPS_SWE = 0, PPS_SCA, PPS_SURFACE_HEAT, PPS_NB, PPS_SP0, PPS_SW0 = PPS_SP0 + HBV_MAX_BINS,
+    PPS_ALB0 = PPS_SW0 + HBV_MAX_BINS, PPS_ISO0 = PPS_ALB0 + HBV_MAX_BINS, PPS_KIRCHNER_Q = PPS_ISO0 + HBV_MAX_BINS,
+    PTHPSK_NS
+};
+// pt_hps_k state-collector series (pt_hps_k_cell_model.h:160-232)
+enum pthpsk_state_series_index {
+    PPC_KIRCHNER = 0, PPC_SCA, PPC_SWE, PPC_SURFACE_HEAT, PPC_SP0, PPC_SW0 = PPC_SP0 + HBV_MAX_BINS,
+    PPC_ALB0 = PPC_SW0 + HBV_MAX_BINS, PPC_ISO0 = PPC_ALB0 + HBV_MAX_BINS, PTHPSK_NSC = PPC_ISO0 + HBV_MAX_BINS
+};
+
 // per-cell error codes written by the stack kernels
 enum cell_error { ERR_NONE = 0, ERR_KIRCHNER_MAX_ITER = 1, ERR_NEGATIVE_OUTFLOW = 2, ERR_SKAUGEN_BISECT = 3,
                   ERR_SKAUGEN_PDF = 4 };

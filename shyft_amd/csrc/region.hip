@@ -169,21 +169,27 @@ struct shyft_hip_region {
     bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
     bool ptssk() const { return stack == SHYFT_HIP_PT_SS_K; }
     bool pthsk() const { return stack == SHYFT_HIP_PT_HS_K; }
+    bool pthpsk() const { return stack == SHYFT_HIP_PT_HPS_K; }
     size_t n_series() const {
         if (collect == COLLECT_ALL) return hbv() ? HBV_NR : PTGSK_NR;
         return collect == COLLECT_DISCHARGE_SNOW ? 4 : 2;
     }
     size_t n_state_fields() const {
-        return hbv() ? HBV_NS : (ptssk() ? PTSSK_NS : (pthsk() ? PTHSK_NS : PTGSK_NS));
+        return hbv() ? HBV_NS : (ptssk() ? PTSSK_NS : (pthsk() ? PTHSK_NS : (pthpsk() ? PTHPSK_NS : PTGSK_NS)));
     }
     // state-collector series per cell (pt_ss_k collects 7 series from its 8 state values)
-    size_t n_state_series() const { return ptssk() ? PTSSK_NSC : (pthsk() ? PTHSK_NSC : n_state_fields()); }
-    size_t n_ref_params() const {
-        return hbv() ? HBV_NP_REF : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP_REF : PTGSK_NP_REF));
+    size_t n_state_series() const {
+        return ptssk() ? PTSSK_NSC : (pthsk() ? PTHSK_NSC : (pthpsk() ? PTHPSK_NSC : n_state_fields()));
     }
-    size_t param_width() const { return hbv() ? HBV_NP : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP : PTGSK_NP_REF)); }
+    size_t n_ref_params() const {
+        return hbv() ? HBV_NP_REF
+                     : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP_REF : (pthpsk() ? PTHPSK_NP_REF : PTGSK_NP_REF)));
+    }
+    size_t param_width() const {
+        return hbv() ? HBV_NP : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP : (pthpsk() ? PTHPSK_NP : PTGSK_NP_REF)));
+    }
     // hbv_snow quantile distribution (n_bins, s[], intervals[]) in the parameter row, or -1
-    int snow_dist_index() const { return hbv() ? HK_NB : (pthsk() ? PH_NB : -1); }
+    int snow_dist_index() const { return hbv() ? HK_NB : (pthsk() ? PH_NB : (pthpsk() ? PP_NB : -1)); }
 };
 
 namespace {
@@ -270,7 +276,8 @@ void update_derived_hbv(shyft_hip_region* h) {
 void update_derived_ptssk(shyft_hip_region* h) {
     const size_t N = h->n;
     const size_t width = h->param_width();
-    const int k_gm = h->pthsk() ? PH_GM_DIRECT : SK_GM_DIRECT, k_rsv = h->pthsk() ? PH_RSV_DRF : SK_RSV_DRF;
+    const int k_gm = h->pthsk() ? PH_GM_DIRECT : (h->pthpsk() ? PP_GM_DIRECT : SK_GM_DIRECT);
+    const int k_rsv = h->pthsk() ? PH_RSV_DRF : (h->pthpsk() ? PP_RSV_DRF : SK_RSV_DRF);
     std::vector<double> cc(PTGSK_NC * N, 0.0);
     for (size_t i = 0; i < N; ++i) {
         const double* g = &h->geo[i * 11];
@@ -303,7 +310,7 @@ void update_derived(shyft_hip_region* h) {
     if (!h->has_params) throw std::runtime_error("region: parameters not set");
     if (h->dt <= 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
     if (h->hbv()) return update_derived_hbv(h);
-    if (h->ptssk() || h->pthsk()) return update_derived_ptssk(h);
+    if (h->ptssk() || h->pthsk() || h->pthpsk()) return update_derived_ptssk(h);
     const size_t N = h->n;
     const double dt_s = double(h->dt) / 1e6;
     const double dt_in_days = dt_s / 86400.0;
@@ -450,7 +457,7 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
     if (!out) return fail(nullptr, "shyft_hip_region_create: out is null");
     *out = nullptr;
     if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK && stack != SHYFT_HIP_PT_SS_K &&
-        stack != SHYFT_HIP_PT_HS_K)
+        stack != SHYFT_HIP_PT_HS_K && stack != SHYFT_HIP_PT_HPS_K)
         return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
     if (n_cells == 0 || n_cells > (size_t)INT32_MAX) return fail(nullptr, "shyft_hip_region_create: invalid n_cells");
     std::unique_ptr<shyft_hip_region> h(new shyft_hip_region());
@@ -534,6 +541,9 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
         } else if (h->pthsk()) {
             if (n_per_set != PTHSK_NP_REF && n_per_set != PTHSK_NP)
                 throw std::runtime_error("pt_ss_k parameter accessor: .set size missmatch");  // pt_hs_k.h:68 text
+        } else if (h->pthpsk()) {
+            if (n_per_set != PTHPSK_NP_REF && n_per_set != PTHPSK_NP)
+                throw std::runtime_error("pt_ss_k parameter accessor: .set size missmatch");  // pt_hps_k.h:70 text
         } else if (n_per_set != h->n_ref_params()) {
             throw std::runtime_error("PTGSK Parameter Accessor: .set size missmatch");
         }
@@ -959,7 +969,7 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     size_t b = n_steps > 0 ? size_t(start_step) : 0;
     size_t e = n_steps > 0 ? size_t(start_step + n_steps) : h->T;
     check_window(h, b, e - b, "run_cells");
-    if (h->ptssk() || h->pthsk()) {
+    if (h->ptssk() || h->pthsk() || h->pthpsk()) {
         ptssk_kargs a;
         a.n_cells = int(h->n);
         a.step0 = int(b);
@@ -971,6 +981,7 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.step_in_days = dt_s / 86400.0;
         a.dt_hours = dt_s / 3600.0;
         a.t1_hours = dt_s / 3600.0;
+        a.dt_us = double(h->dt);
         a.params = h->d_params.p;
         a.set_ix = h->d_set_ix.p;
         a.cellc = h->d_cellc.p;
@@ -983,7 +994,9 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.active = h->active.empty() ? nullptr : h->d_active.p;
         a.err = h->d_err.p;
         hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
-        if (h->pthsk())
+        if (h->pthpsk())
+            hip_check(launch_pthpsk_run(a, h->stream), "pthpsk_run_kernel launch");
+        else if (h->pthsk())
             hip_check(launch_pthsk_run(a, h->stream), "pthsk_run_kernel launch");
         else
             hip_check(launch_ptssk_run(a, h->stream), "ptssk_run_kernel launch");
@@ -1049,7 +1062,8 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
 static void finish_run(shyft_hip_region* h) {
     hip_check(hipStreamSynchronize(h->stream), h->hbv() ? "hbv_run_kernel"
                                                : h->ptssk() ? "ptssk_run_kernel"
-                                               : h->pthsk() ? "pthsk_run_kernel" : "ptgsk_run_kernel");
+                                               : h->pthsk() ? "pthsk_run_kernel"
+                                               : h->pthpsk() ? "pthpsk_run_kernel" : "ptgsk_run_kernel");
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
     h->last_ms = ms;

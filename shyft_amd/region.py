@@ -12,7 +12,7 @@ import numpy as np
 
 from ._native import check, lib
 
-PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K = 1, 2, 3, 4
+PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K, PT_HPS_K = 1, 2, 3, 4, 5
 TEMPERATURE, PRECIPITATION, WIND_SPEED, REL_HUM, RADIATION = range(5)
 FORCING_NAMES = ("temperature", "precipitation", "wind_speed", "rel_hum", "radiation")
 COLLECT_DISCHARGE, COLLECT_DISCHARGE_SNOW, COLLECT_ALL = 0, 1, 2
@@ -35,10 +35,18 @@ PTHSK_STATE = (("swe", "sca", "n_bins") + tuple(f"sp{i}" for i in range(HBV_MAX_
                tuple(f"sw{i}" for i in range(HBV_MAX_BINS)) + ("kirchner_q",))
 PTHSK_STATE_SERIES = (("kirchner_discharge", "snow_sca", "snow_swe") + tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) +
                       tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
-STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22, PT_SS_K: 21, PT_HS_K: 18}
-STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE), PT_SS_K: len(PTSSK_STATE), PT_HS_K: len(PTHSK_STATE)}
+# pt_hps_k (core/pt_hps_k.h:163-185, pt_hps_k_cell_model.h:160-232); response series ids are the pt_gs_k ones
+_B = tuple(range(HBV_MAX_BINS))
+PTHPSK_STATE = (("swe", "sca", "surface_heat", "n_bins") + tuple(f"sp{i}" for i in _B) + tuple(f"sw{i}" for i in _B) +
+                tuple(f"albedo{i}" for i in _B) + tuple(f"iso_pot_energy{i}" for i in _B) + ("kirchner_q",))
+PTHPSK_STATE_SERIES = (("kirchner_discharge", "hps_sca", "hps_swe", "hps_surface_heat") +
+                       tuple(f"sp{i}" for i in _B) + tuple(f"sw{i}" for i in _B) + tuple(f"albedo{i}" for i in _B) +
+                       tuple(f"iso_pot_energy{i}" for i in _B))
+STACK_NPARAM = {PT_GS_K: 31, HBV_STACK: 22, PT_SS_K: 21, PT_HS_K: 18, PT_HPS_K: 24}
+STACK_NSTATE = {PT_GS_K: 9, HBV_STACK: len(HBV_STATE), PT_SS_K: len(PTSSK_STATE), PT_HS_K: len(PTHSK_STATE),
+                PT_HPS_K: len(PTHPSK_STATE)}
 STACK_NSERIES = {PT_GS_K: len(PTGSK_SERIES), HBV_STACK: len(HBV_SERIES), PT_SS_K: len(PTGSK_SERIES),
-                 PT_HS_K: len(PTGSK_SERIES)}
+                 PT_HS_K: len(PTGSK_SERIES), PT_HPS_K: len(PTGSK_SERIES)}
 
 
 def _ptr(a: np.ndarray | None):

@@ -219,3 +219,33 @@ def default_pthsk_state(n_cells: int, q: float = 1.0, swe: float = 0.0, sca: flo
     s[:, 1] = sca
     s[:, -1] = q
     return s
+
+
+def default_pthpsk_parameters() -> np.ndarray:
+    """PTHPSKParameter() defaults in the reference get/set order (core/pt_hps_k.h:64-90)."""
+    return np.array([
+        -2.439, 0.966, -0.10,            # kirchner c1 c2 c3
+        1.5,                             # ae.ae_scale_factor
+        0.1, 0.0, 0.5,                   # hps lw tx cfr (hbv_physical_snow.h:45-47)
+        2.0, 1.0, 30.0,                  # hps wind_scale wind_const surface_magnitude
+        0.9, 0.6, 5.0, 5.0, 5.0,         # hps max/min albedo, fast/slow albedo decay rate, snowfall_reset_depth
+        0.0,                             # hps.calculate_iso_pot_energy
+        6.0,                             # gm.dtf
+        1.0,                             # p_corr.scale_factor
+        0.2, 1.26,                       # pt.albedo pt.alpha
+        1.0, 7.0, 0.0,                   # routing velocity alpha beta
+        1.0,                             # msp.reservoir_direct_response_fraction
+    ], dtype=np.float64)
+
+
+PTHPSK_NS = 4 + 4 * HBV_MAX_BINS + 1  # swe sca surface_heat n_bins sp[8] sw[8] albedo[8] iso_pot_energy[8] kirchner.q
+
+
+def default_pthpsk_state(n_cells: int, q: float = 1.0, swe: float = 0.0, sca: float = 0.0) -> np.ndarray:
+    """PTHPSKState(): hbv_physical_snow::state() (surface_heat 30000, undistributed) with kirchner.q = q."""
+    s = np.zeros((n_cells, PTHPSK_NS), dtype=np.float64)
+    s[:, 0] = swe
+    s[:, 1] = sca
+    s[:, 2] = 30000.0
+    s[:, -1] = q
+    return s

@@ -159,3 +159,43 @@ def run_pthsk(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0,
         return out
     finally:
         r.close()
+
+
+def run_pthpsk(engine, geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None,
+               gm_direct=None, snow_dist=None, full=True, collect_state=False):
+    """pt_hps_k region; forcing [5][T][N]; params [n_sets][24]; state [N][37].
+    Returns dict main [2][T][N], full [8][T][N], state [N][37] (+ state_series [36][T+1][N])."""
+    geo11 = np.atleast_2d(geo11)
+    if engine == "oracle":
+        return oracle_lib.pthpsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step, n_steps, set_ix,
+                                     gm_direct=gm_direct, snow_dist=snow_dist, full=full, collect_state=collect_state)
+    from shyft_amd.region import HipRegion, PT_HPS_K, COLLECT_ALL, COLLECT_DISCHARGE, PTHPSK_STATE, PTHPSK_STATE_SERIES
+    N = geo11.shape[0]
+    T = forcing.shape[1]
+    p = np.atleast_2d(np.asarray(params, dtype=np.float64))
+    if gm_direct is not None or snow_dist is not None:  # the 42-wide C-ABI row: + gm.direct_response + distribution
+        gm = np.zeros((p.shape[0], 1)) if gm_direct is None else np.asarray(gm_direct, dtype=np.float64).reshape(-1, 1)
+        d = (np.tile(oracle_lib.hbv_dist_row([1.0] * 5, [0.0, 0.25, 0.5, 0.75, 1.0]), (p.shape[0], 1))
+             if snow_dist is None else np.atleast_2d(snow_dist))
+        p = np.concatenate([p, gm, d], axis=1)
+    r = HipRegion(PT_HPS_K, N)
+    try:
+        r.set_geo(geo11)
+        r.set_parameters(p, set_ix)
+        r.set_time_axis(t0_us, dt_us, T)
+        r.set_collection(COLLECT_ALL if full else COLLECT_DISCHARGE, collect_state)
+        r.set_state(np.asarray(state).reshape(N, len(PTHPSK_STATE)))
+        for v in range(5):
+            r.set_forcing(v, 0, forcing[v])
+        r.run_cells(0, start_step, n_steps)
+        out = {"state": r.get_state()}
+        ns = 8 if full else 2
+        allser = np.stack([r.get_series(k, 0, T) for k in range(ns)])
+        out["main"] = allser[:2]
+        if full:
+            out["full"] = allser
+        if collect_state:
+            out["state_series"] = np.stack([r.get_state_series(k, 0, T + 1) for k in range(len(PTHPSK_STATE_SERIES))])
+        return out
+    finally:
+        r.close()

@@ -315,3 +315,62 @@ def pthsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps
     if collect_state:
         r["state_series"] = out_state
     return r
+
+
+PTHPSK_FLAT = 4 + 4 * HBV_MAX_BINS + 1  # swe sca surface_heat n_bins sp[8] sw[8] albedo[8] iso_pot_energy[8] q
+PTHPSK_NSC = 4 + 4 * HBV_MAX_BINS       # kirchner_discharge hps_sca hps_swe hps_surface_heat sp sw albedo iso
+
+
+def hps_step(st36, p12, dist17, distribute, dt_us, T, rad, prec_mm_h, wind_speed, rel_hum, variant="detmath"):
+    """One hbv_physical_snow step on a flat state (updated in place). Returns (outflow, sca, storage)."""
+    L = load(variant)
+    L.oracle_hps_step.restype = C.c_int
+    L.oracle_hps_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64] + \
+        [C.c_double] * 5 + [C.c_char_p, C.c_size_t]
+    st = np.ascontiguousarray(st36, dtype=np.float64)
+    p = np.ascontiguousarray(p12, dtype=np.float64)
+    d = np.ascontiguousarray(dist17, dtype=np.float64)
+    r = np.zeros(3)
+    err = C.create_string_buffer(512)
+    if L.oracle_hps_step(_p(st), _p(r), _p(p), _p(d), int(distribute), int(dt_us), float(T), float(rad),
+                         float(prec_mm_h), float(wind_speed), float(rel_hum), err, 512) != 0:
+        raise RuntimeError(err.value.decode())
+    st36[:] = st
+    return tuple(r)
+
+
+def pthpsk_run(geo11, params, state, t0_us, dt_us, forcing, start_step=0, n_steps=0, set_ix=None, gm_direct=None,
+               snow_dist=None, full=False, collect_state=False, ncore=0, variant="detmath"):
+    """Run the oracle pt_hps_k region. params [n_sets][24]; gm_direct [n_sets] or None; snow_dist [n_sets][17] or
+    None; state [N][37]. Returns dict main [2][T][N], full [8][T][N], state_series [36][T+1][N], state [N][37]."""
+    L = load(variant)
+    L.oracle_pthpsk_run.restype = C.c_int
+    L.oracle_pthpsk_run.argtypes = ([C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                     C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_size_t, C.c_int, C.c_int] +
+                                    [C.c_void_p] * 8 + [C.c_int, C.POINTER(C.c_double), C.c_char_p, C.c_size_t])
+    geo11 = np.ascontiguousarray(geo11, dtype=np.float64)
+    N = geo11.shape[0]
+    params = np.ascontiguousarray(np.atleast_2d(params), dtype=np.float64)
+    gm = None if gm_direct is None else np.ascontiguousarray(np.atleast_1d(gm_direct), dtype=np.float64)
+    dist = None if snow_dist is None else np.ascontiguousarray(np.atleast_2d(snow_dist), dtype=np.float64)
+    st = np.ascontiguousarray(state, dtype=np.float64).reshape(N, PTHPSK_FLAT).copy()
+    F = np.ascontiguousarray(forcing, dtype=np.float64)
+    T = F.shape[1]
+    ix = None if set_ix is None else np.ascontiguousarray(set_ix, dtype=np.int32)
+    out_main = np.empty((2, T, N))
+    out_full = np.empty((8, T, N)) if full else None
+    out_state = np.empty((PTHPSK_NSC, T + 1, N)) if collect_state else None
+    el = C.c_double(0.0)
+    err = C.create_string_buffer(512)
+    rc = L.oracle_pthpsk_run(N, _p(geo11), _p(params), _p(gm), _p(dist), params.shape[0], _p(ix), _p(st),
+                             int(t0_us), int(dt_us), T, int(start_step), int(n_steps), _p(F[0]), _p(F[1]), _p(F[2]),
+                             _p(F[3]), _p(F[4]), _p(out_main), _p(out_full), _p(out_state), int(ncore), C.byref(el),
+                             err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    r = {"main": out_main, "state": st, "elapsed_s": el.value}
+    if full:
+        r["full"] = out_full
+    if collect_state:
+        r["state_series"] = out_state
+    return r

@@ -39,14 +39,14 @@ def test_state_blob_roundtrip_and_stack_tag():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stack", ["pt_gs_k", "hbv_stack", "pt_ss_k", "pt_hs_k"])
+@pytest.mark.parametrize("stack", ["pt_gs_k", "hbv_stack", "pt_ss_k", "pt_hs_k", "pt_hps_k"])
 def test_verify_state_handler(stack):
     """verify_state_handler (test_region_model_stacks.py:71-78) for every stack's model."""
     import importlib
     from shyft_amd import api
     from tests.test_api_region_model import build_model
     m = importlib.import_module(f"shyft_amd.api.{stack}")
-    pre = {"pt_gs_k": "PTGSK", "hbv_stack": "Hbv", "pt_ss_k": "PTSSK", "pt_hs_k": "PTHSK"}[stack]
+    pre = {"pt_gs_k": "PTGSK", "hbv_stack": "Hbv", "pt_ss_k": "PTSSK", "pt_hs_k": "PTHSK", "pt_hps_k": "PTHPSK"}[stack]
     model = build_model(getattr(m, pre + "Model"), getattr(m, pre + "Parameter"), 20)
     cids = api.IntVector()
     states = model.state.extract_state(cids)
