@@ -69,6 +69,8 @@ def parse():
                          "per chunk the (river, UHG)-group sums are formed on each GPU and all-gathered, after the "
                          "last chunk the network is convolved on the device (on by default for --stack pt_ss_k)")
     ap.add_argument("--no-routing", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one region: generate each chunk's forcing, then run it (no generator/kernel overlap)")
     ap.add_argument("--chunk", type=int, default=CHUNK)
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
@@ -197,6 +199,7 @@ class Router:
         _, _, group = synthetic.cell_routing(cells, self.n_catch, cell_offset=rank * cells, n_total=world * cells)
         self.G = self.n_catch * len(synthetic.ROUTE_DISTANCES)
         r.set_routing_groups(group, self.G)
+        self.group = group
         self.rivers = synthetic.river_network(self.n_catch)
         steps = [int((d / 1.0) / 3600.0 + 0.5) for d in synthetic.ROUTE_DISTANCES]
         self.group_uhgs = [api.make_uhg_from_gamma(steps[k], 7.0, 0.0) for _ in range(self.n_catch)
@@ -209,6 +212,9 @@ class Router:
         self.part = None
         self.pg = pg
         self.out = None
+
+    def attach(self, r):
+        r.set_routing_groups(self.group, self.G)
 
     def chunk(self, r, step0, n):
         import torch
@@ -229,9 +235,17 @@ class Router:
         return self.out
 
 
-def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router=None, btk=False, btk_ms=None):
+def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router=None, btk=False, btk_ms=None,
+             r_alt=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
-    or IDW / BTK from the station network), then run_cells (and the routing group sums)."""
+    or IDW / BTK from the station network), then run_cells (and the routing group sums).
+
+    With r_alt (a second region over the same cells) and the device generator, the chunks alternate between
+    the two regions: chunk s+1's forcing is generated into the other region's window on its own stream while
+    chunk s runs, and the state is handed over device to device (shyft_hip_copy_state) before chunk s+1 runs.
+    Every chunk's forcing is still produced inside the timed region; the generator just no longer adds to it."""
+    if r_alt is not None and stations is None:
+        return _run_year_pipelined((r, r_alt), cells, rank, chunk, k_steps, seed, state0, router)
     kernel_ms = []
     r.set_state(state0)
     for s in range(k_steps):
@@ -256,6 +270,30 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router
         kernel_ms.append(r.last_run_ms())
         if router is not None:
             router.chunk(r, step0, chunk)
+    if router is not None:
+        router.finish(k_steps * chunk)
+    return kernel_ms
+
+
+def _run_year_pipelined(regs, cells, rank, chunk, k_steps, seed, state0, router):
+    kernel_ms = []
+    regs[0].set_state(state0)
+    regs[0].move_window(0, 0)
+    regs[0].synthetic_forcing(seed, 0, chunk, cell_offset=rank * cells)
+    for s in range(k_steps):
+        cur, nxt = regs[s % 2], regs[(s + 1) % 2]
+        step0 = s * chunk
+        cur.run_cells_async(step0, chunk)
+        if s + 1 < k_steps:
+            # host-synchronous on nxt's stream only: the generator overlaps cur's kernel
+            nxt.move_window(step0 + chunk, 0)
+            nxt.synthetic_forcing(seed, step0 + chunk, chunk, cell_offset=rank * cells)
+        cur.synchronize()   # error check of the run (region_model::run_cells semantics)
+        kernel_ms.append(cur.last_run_ms())
+        if s + 1 < k_steps:
+            nxt.copy_state_from(cur)
+        if router is not None:
+            router.chunk(cur, step0, chunk)
     if router is not None:
         router.finish(k_steps * chunk)
     return kernel_ms
@@ -344,14 +382,20 @@ def main():
 
     routing = (a.routing or a.stack == "pt_ss_k") and not a.no_routing
     router = Router(r, cells, world, rank, local, n_axis, pg) if routing else None
+    r_alt = None
+    if not a.idw and not a.no_pipeline:
+        r_alt = build_region(a.stack, cells, world, rank, local, chunk, n_axis)
+        if router is not None:
+            router.attach(r_alt)
 
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
-        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations, router, a.btk)
+        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations, router, a.btk, r_alt=r_alt)
     barrier_sync(pg, local)
     t0 = time.perf_counter()
     btk_ms = []
-    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations, router, a.btk, btk_ms)
+    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations, router, a.btk, btk_ms,
+                         r_alt=r_alt)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
@@ -388,6 +432,10 @@ def main():
             "cells_per_gpu": cells,
             "total_cells": world * cells,
             "steps_per_chunk": chunk,
+            "forcing": ("IDW/BTK from stations, per chunk, before its run" if a.idw else
+                        "device generator, per chunk, overlapped with the previous chunk's run (two regions, state "
+                        "handed over device to device)" if r_alt is not None else
+                        "device generator, per chunk, before its run"),
             "parallelism": f"cells sharded over {world} GPU(s), no data-path collective",
         },
         "kernel_ms_per_step": avg_kernel_ms,
@@ -448,6 +496,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     r.close()
+    if r_alt is not None:
+        r_alt.close()
     if pg is not None:
         pg.destroy_process_group()
 

@@ -111,6 +111,10 @@ int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, siz
  * get/set_states (region_model.h:784-805). */
 int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_fields);
 int shyft_hip_get_state(const shyft_hip_region* h, double* state, size_t n_fields);
+/* dst's state := src's state, device to device (the same method stack and cell count, one device).
+ * Replaces dst.set_states(src.get_states()) (region_model.h:784-805) without the host round trip: waits for
+ * src's queued work, then copies on dst's stream. Used to pipeline two regions over consecutive windows. */
+int shyft_hip_copy_state(shyft_hip_region* dst, const shyft_hip_region* src);
 
 /* Forcing for steps [step0, step0+n) of one variable, [n][n_cells].
  * src_on_device != 0: src is a device pointer on the region's device. */

@@ -34,6 +34,7 @@ SIGNATURES = {
     "shyft_hip_set_catchment_filter": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_set_state": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_get_state": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
+    "shyft_hip_copy_state": (C.c_int, [_h, _h]),
     "shyft_hip_set_forcing": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
     "shyft_hip_get_forcing": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
     "shyft_hip_synthetic_forcing": (C.c_int, [_h, C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t]),

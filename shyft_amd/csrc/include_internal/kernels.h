@@ -124,6 +124,8 @@ hipError_t launch_gather_columns(double* dst, const double* src, size_t n_rows, 
                                  size_t n_lanes, hipStream_t stream);
 
 // flag = 1 if any of rows x cells (restricted to active cells when active != null) is NaN
+// first[0] = min(first[0], lowest i with err[i] != 0); caller initialises first[0] to a value >= n
+hipError_t launch_first_error(const int32_t* err, size_t n, int32_t* first, hipStream_t stream);
 hipError_t launch_nan_scan(const double* f, size_t n_rows, size_t n_cells, const uint8_t* active, int32_t* flag,
                            hipStream_t stream);
 

@@ -83,6 +83,12 @@ __global__ void nan_scan_kernel(const double* __restrict__ f, size_t n_rows, siz
     if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1;
 }
 
+// Lowest cell index whose run error code is non-zero (errors are rare: one atomic per failing lane).
+__global__ void first_error_kernel(const int32_t* __restrict__ err, size_t n, int32_t* __restrict__ first) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        if (err[i]) atomicMin(first, (int32_t)i);
+}
+
 __global__ void fill_kernel(double* __restrict__ p, size_t n, double v) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -129,6 +135,14 @@ hipError_t launch_fill(double* p, size_t n, double v, hipStream_t stream) {
     size_t blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(fill_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_first_error(const int32_t* err, size_t n, int32_t* first, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(first_error_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, err, n, first);
     return hipGetLastError();
 }
 

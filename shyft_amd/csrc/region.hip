@@ -689,6 +689,21 @@ int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_field
     });
 }
 
+int shyft_hip_copy_state(shyft_hip_region* dst, const shyft_hip_region* src) {
+    if (!dst || !src) return fail(dst, "shyft_hip_copy_state: null argument");
+    return guarded(dst, [&] {
+        if (src->stack != dst->stack || src->n != dst->n)
+            throw std::runtime_error("copy_state: regions differ in method stack or number of cells");
+        if (!src->has_state) throw std::runtime_error("copy_state: source region has no state");
+        // ordered after everything already queued on the source stream; the copy itself runs on the
+        // destination stream, so the destination's next run starts after it without a host wait
+        hip_check(hipStreamSynchronize(src->stream), "copy_state: source stream");
+        hip_check(hipMemcpyAsync(dst->d_state.p, src->d_state.p, dst->n_state_fields() * dst->n * sizeof(double),
+                                 hipMemcpyDeviceToDevice, dst->stream), "copy_state");
+        dst->has_state = true;
+    });
+}
+
 int shyft_hip_get_state(const shyft_hip_region* hc, double* state, size_t n_fields) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !state) return fail(h, "shyft_hip_get_state: null argument");
@@ -1067,25 +1082,29 @@ static void finish_run(shyft_hip_region* h) {
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
     h->last_ms = ms;
-    std::vector<int32_t> errs(h->n);
-    // cheap check: reduce on host only when the kernel flagged something
-    hip_check(hipMemcpy(errs.data(), h->d_err.p, h->n * sizeof(int32_t), hipMemcpyDeviceToHost), "download err");
-    for (size_t i = 0; i < h->n; ++i)
-        if (errs[i]) {
-            hip_check(hipMemset(h->d_err.p, 0, h->n * sizeof(int32_t)), "memset");
-            if (errs[i] == ERR_NEGATIVE_OUTFLOW)
-                throw std::runtime_error("Negative outflow: total_water - swe < -1e-6 in hbv_snow (cell " +
-                                         std::to_string(i) + ")");
-            if (errs[i] == ERR_SKAUGEN_BISECT)
-                throw std::runtime_error("No change of sign in boost::math::tools::bisect, either there is no root to "
-                                         "find, or there are multiple roots in the interval (skaugen sca_rel_red, cell " +
-                                         std::to_string(i) + ")");
-            if (errs[i] == ERR_SKAUGEN_PDF)
-                throw std::runtime_error("boost::math::pdf(gamma_distribution): overflow at x = 0 (skaugen sca_rel_red, "
-                                         "cell " + std::to_string(i) + ")");
-            throw std::runtime_error("kirchner: Max number of iterations exceeded (500). A new step size was not found. (cell " +
-                                     std::to_string(i) + ")");
-        }
+    // the per-cell error codes stay on the device: one reduction to the lowest failing cell, 8 bytes back
+    const int32_t none = INT32_MAX;
+    hip_check(hipMemcpyAsync(h->d_flag.p, &none, sizeof(int32_t), hipMemcpyHostToDevice, h->stream), "upload flag");
+    hip_check(launch_first_error(h->d_err.p, h->n, h->d_flag.p, h->stream), "first_error");
+    int32_t first = none;
+    hip_check(hipMemcpyAsync(&first, h->d_flag.p, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), "download flag");
+    hip_check(hipStreamSynchronize(h->stream), "first_error");
+    if (first == none) return;
+    const size_t i = size_t(first);
+    int32_t code = 0;
+    hip_check(hipMemcpy(&code, h->d_err.p + i, sizeof(int32_t), hipMemcpyDeviceToHost), "download err");
+    hip_check(hipMemset(h->d_err.p, 0, h->n * sizeof(int32_t)), "memset");
+    if (code == ERR_NEGATIVE_OUTFLOW)
+        throw std::runtime_error("Negative outflow: total_water - swe < -1e-6 in hbv_snow (cell " + std::to_string(i) + ")");
+    if (code == ERR_SKAUGEN_BISECT)
+        throw std::runtime_error("No change of sign in boost::math::tools::bisect, either there is no root to "
+                                 "find, or there are multiple roots in the interval (skaugen sca_rel_red, cell " +
+                                 std::to_string(i) + ")");
+    if (code == ERR_SKAUGEN_PDF)
+        throw std::runtime_error("boost::math::pdf(gamma_distribution): overflow at x = 0 (skaugen sca_rel_red, "
+                                 "cell " + std::to_string(i) + ")");
+    throw std::runtime_error("kirchner: Max number of iterations exceeded (500). A new step size was not found. (cell " +
+                             std::to_string(i) + ")");
 }
 
 int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {

@@ -120,6 +120,10 @@ class HipRegion:
         self._chk(self._L.shyft_hip_get_state(self.h, _ptr(s), nf))
         return s
 
+    def copy_state_from(self, src: "HipRegion"):
+        """This region's state := src's state, device to device (same stack and cell count)."""
+        self._chk(self._L.shyft_hip_copy_state(self.h, src.h))
+
     def set_forcing(self, var: int, step0: int, values: np.ndarray):
         v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self.n)
         self._chk(self._L.shyft_hip_set_forcing(self.h, var, step0, v.shape[0], _ptr(v), 0))

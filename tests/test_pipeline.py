@@ -1,0 +1,93 @@
+"""Two regions pipelined over consecutive windows (shyft_hip_copy_state + run_cells_async, as bench.py runs the
+year) give bit-identical discharge and final state to one region running the chunks in order; the device-side
+error reduction of run_cells still reports the lowest failing cell."""
+import numpy as np
+import pytest
+
+from shyft_amd import synthetic
+from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, COLLECT_DISCHARGE
+
+Q_AVG = 0  # avg_discharge series
+
+pytestmark = pytest.mark.gpu
+
+CHUNK, K, N = 48, 5, 3000
+
+
+def _region(stack, params):
+    r = HipRegion(stack, N, device=0)
+    r.set_geo(synthetic.geo11(N, n_catchments=4))
+    r.set_parameters(params)
+    r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, CHUNK * K, CHUNK)
+    r.set_collection(COLLECT_DISCHARGE)
+    return r
+
+
+@pytest.mark.parametrize("stack", [PT_GS_K, HBV_STACK])
+def test_pipelined_regions_match_sequential(stack):
+    if stack == PT_GS_K:
+        p, st = synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(N)
+    else:
+        p, st = synthetic.default_hbv_parameters(), synthetic.default_hbv_state(N)
+    seq = _region(stack, p)
+    seq.set_state(st)
+    q_seq = []
+    for s in range(K):
+        seq.move_window(s * CHUNK, 0)
+        seq.synthetic_forcing(synthetic.SEED, s * CHUNK, CHUNK)
+        seq.run_cells(0, s * CHUNK, CHUNK)
+        q_seq.append(seq.get_series(Q_AVG, s * CHUNK, CHUNK))
+    regs = (_region(stack, p), _region(stack, p))
+    regs[0].set_state(st)
+    regs[0].move_window(0, 0)
+    regs[0].synthetic_forcing(synthetic.SEED, 0, CHUNK)
+    q_pipe = []
+    for s in range(K):
+        cur, nxt = regs[s % 2], regs[(s + 1) % 2]
+        cur.run_cells_async(s * CHUNK, CHUNK)
+        if s + 1 < K:
+            nxt.move_window((s + 1) * CHUNK, 0)
+            nxt.synthetic_forcing(synthetic.SEED, (s + 1) * CHUNK, CHUNK)
+        cur.synchronize()
+        q_pipe.append(cur.get_series(Q_AVG, s * CHUNK, CHUNK))
+        if s + 1 < K:
+            nxt.copy_state_from(cur)
+    assert np.array_equal(np.concatenate(q_seq), np.concatenate(q_pipe))
+    assert np.array_equal(seq.get_state(), regs[(K - 1) % 2].get_state())
+    other = _region(PT_GS_K if stack == HBV_STACK else HBV_STACK,
+                    synthetic.default_hbv_parameters() if stack == PT_GS_K else synthetic.default_ptgsk_parameters())
+    with pytest.raises(RuntimeError, match="differ in method stack"):
+        other.copy_state_from(seq)
+    for r in (seq, *regs, other):
+        r.close()
+
+
+def test_run_error_reports_lowest_failing_cell():
+    """The reference's hbv_physical_snow 'Negative outflow' (test_pthpsk.py skewed-distribution case) planted in a
+    few cells through a second parameter set: the message names the lowest cell the oracle fails on."""
+    from shyft_amd._native import ShyftHipError
+    from tests import engines, oracle_lib
+    from tests.test_pthpsk import _case, HOUR
+    n, T = 64, 24 * 40
+    geo, f = _case(n, T, step0=24 * 50, seed=9)
+    a5 = [0.0, 0.25, 0.5, 0.75, 1.0]
+    i1 = [0.0, 0.2, 0.5, 0.8, 1.0]
+    good = oracle_lib.hbv_dist_row(oracle_lib.hbv_normalize([1.0] * 5, a5), a5)
+    skew = oracle_lib.hbv_dist_row(oracle_lib.hbv_normalize([0.5, 0.8, 1.0, 1.3, 1.5], i1), i1)
+    p = synthetic.default_pthpsk_parameters()
+    st = synthetic.default_pthpsk_state(n, q=2.0)
+    planted = [41, 17, 58]
+    failing = []
+    for c in sorted(planted):
+        try:
+            engines.run_pthpsk("oracle", geo[c:c + 1], p, st[c:c + 1], synthetic.T0_2015_US, HOUR,
+                               np.ascontiguousarray(f[:, :, c:c + 1]), snow_dist=skew)
+        except RuntimeError:
+            failing.append(c)
+    if not failing:
+        pytest.skip("the skewed distribution did not fail in any planted cell")
+    ix = np.zeros(n, np.int32)
+    ix[planted] = 1
+    with pytest.raises(ShyftHipError, match=f"Negative outflow.*cell {min(failing)}\\)"):
+        engines.run_pthpsk("hip", geo, np.stack([p, p]), st, synthetic.T0_2015_US, HOUR, f, set_ix=ix,
+                           snow_dist=np.stack([good, skew]))
