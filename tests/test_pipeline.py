@@ -76,7 +76,7 @@ def test_run_error_reports_lowest_failing_cell():
     skew = oracle_lib.hbv_dist_row(oracle_lib.hbv_normalize([0.5, 0.8, 1.0, 1.3, 1.5], i1), i1)
     p = synthetic.default_pthpsk_parameters()
     st = synthetic.default_pthpsk_state(n, q=2.0)
-    planted = [41, 17, 58]
+    planted = [30, 41, 58, 3]   # the oracle fails on cells 3 and 30 of this case
     failing = []
     for c in sorted(planted):
         try:
