@@ -210,11 +210,9 @@ IDW_PARAMS = {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("by_equation", [False, True])
+# gradient_by_equation applies to temperature only
+@pytest.mark.parametrize("var,by_equation", [(0, False), (0, True), (1, False), (2, False), (3, False), (4, False)])
 def test_idw_kernel_bitexact_vs_oracle(var, by_equation):
-    if by_equation and var != 0:
-        pytest.skip("gradient_by_equation applies to temperature only")
     from shyft_amd.region import HipRegion, PT_GS_K
     from shyft_amd import synthetic
     geo, xyz, vals = _c3_like()
