@@ -20,7 +20,17 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-__global__ __launch_bounds__(BLOCK) void hbv_run_kernel(const hbv_kargs a) {
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_HBV_WAVES=N, 0 = the compiler's choice)
+#ifndef SHYFT_HBV_WAVES
+#define SHYFT_HBV_WAVES 3  // measured: compiler choice (2) 19.2 ms, 3: 18.5, 4: 20.8
+#endif
+#if SHYFT_HBV_WAVES > 0
+#define SHYFT_HBV_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_HBV_WAVES, SHYFT_HBV_WAVES)))
+#else
+#define SHYFT_HBV_OCC
+#endif
+
+__global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;

@@ -24,7 +24,17 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-__global__ __launch_bounds__(BLOCK) void pthpsk_run_kernel(const pthpsk_kargs a) {
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTHPSK_WAVES=N, 0 = the compiler's choice)
+#ifndef SHYFT_PTHPSK_WAVES
+#define SHYFT_PTHPSK_WAVES 2  // measured: compiler choice (1) 151 ms, 2: 91, 3: 123
+#endif
+#if SHYFT_PTHPSK_WAVES > 0
+#define SHYFT_PTHPSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHPSK_WAVES, SHYFT_PTHPSK_WAVES)))
+#else
+#define SHYFT_PTHPSK_OCC
+#endif
+
+__global__ __launch_bounds__(BLOCK) SHYFT_PTHPSK_OCC void pthpsk_run_kernel(const pthpsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;

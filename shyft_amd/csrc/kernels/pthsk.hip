@@ -24,7 +24,17 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-__global__ __launch_bounds__(BLOCK) void pthsk_run_kernel(const pthsk_kargs a) {
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTHSK_WAVES=N, 0 = the compiler's choice)
+#ifndef SHYFT_PTHSK_WAVES
+#define SHYFT_PTHSK_WAVES 3  // measured: compiler choice (1) 123 ms, 2: 70, 3: 64, 4: 70 per 730-step chunk
+#endif
+#if SHYFT_PTHSK_WAVES > 0
+#define SHYFT_PTHSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHSK_WAVES, SHYFT_PTHSK_WAVES)))
+#else
+#define SHYFT_PTHSK_OCC
+#endif
+
+__global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const pthsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;

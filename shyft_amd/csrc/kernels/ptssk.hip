@@ -23,7 +23,17 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-__global__ __launch_bounds__(BLOCK) void ptssk_run_kernel(const ptssk_kargs a) {
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTSSK_WAVES=N, 0 = the compiler's choice)
+#ifndef SHYFT_PTSSK_WAVES
+#define SHYFT_PTSSK_WAVES 4  // measured: compiler choice (2) 188 ms, 3: 153, 4: 145, 5: 143, 6: 142
+#endif
+#if SHYFT_PTSSK_WAVES > 0
+#define SHYFT_PTSSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTSSK_WAVES, SHYFT_PTSSK_WAVES)))
+#else
+#define SHYFT_PTSSK_OCC
+#endif
+
+__global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const ptssk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;
