@@ -20,9 +20,13 @@ namespace {
 
 constexpr int BLOCK = 256;
 
+#ifndef SHYFT_HBV_PREFETCH
+#define SHYFT_HBV_PREFETCH 1
+#endif
+
 // occupancy target (waves per SIMD; variant builds override with -DSHYFT_HBV_WAVES=N, 0 = the compiler's choice)
 #ifndef SHYFT_HBV_WAVES
-#define SHYFT_HBV_WAVES 3  // measured: compiler choice (2) 19.2 ms, 3: 18.5, 4: 20.8
+#define SHYFT_HBV_WAVES 2  // measured without the forcing prefetch: compiler choice (2) 19.2 ms, 3: 18.5, 4: 20.8; with it: 2: 14.9, 3: 16.3, 4: 23.1
 #endif
 #if SHYFT_HBV_WAVES > 0
 #define SHYFT_HBV_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_HBV_WAVES, SHYFT_HBV_WAVES)))
@@ -110,14 +114,28 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     };
 
     const int i_end = a.step0 + a.n_steps;
+    // the next step's forcing is loaded before this step's arithmetic, so its HBM latency overlaps the step
+    // instead of stalling the top of every iteration (the kernel is latency-bound at 3 waves per SIMD)
+    double nx_temp = 0, nx_rad = 0, nx_rh = 0, nx_prec = 0;
+    if (SHYFT_HBV_PREFETCH && a.step0 < i_end) {
+        const size_t ff = (size_t)(a.step0 - a.win0) * NF + fcl;
+        nx_temp = f_temp[ff]; nx_rad = f_rad[ff]; nx_rh = f_rh[ff]; nx_prec = f_prec[ff];
+    }
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
-        const size_t ff = wi * NF + fcl;
-        const double temp = f_temp[ff];
-        const double rad = f_rad[ff];
-        const double rel_hum = f_rh[ff];
-        const double prec = f_prec[ff] * p_corr;
+        double temp, rad, rel_hum, prec_raw;
+        if (SHYFT_HBV_PREFETCH) {
+            temp = nx_temp; rad = nx_rad; rel_hum = nx_rh; prec_raw = nx_prec;
+            if (i + 1 < i_end) {
+                const size_t fn = (wi + 1) * NF + fcl;
+                nx_temp = f_temp[fn]; nx_rad = f_rad[fn]; nx_rh = f_rh[fn]; nx_prec = f_prec[fn];
+            }
+        } else {
+            const size_t ff = wi * NF + fcl;
+            temp = f_temp[ff]; rad = f_rad[ff]; rel_hum = f_rh[ff]; prec_raw = f_prec[ff];
+        }
+        const double prec = prec_raw * p_corr;
         if (SS) collect_state(wi);
         const double snow_outflow =
             hbv_snow_step(sp_par, sp, sw, swe, sca, a.step_in_days, a.dt_hours, prec, temp, err);
