@@ -63,6 +63,19 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=0,
                     help="cells per GPU (default 1,048,576 for pt_gs_k, 524,288 for hbv_stack)")
+    ap.add_argument("--total-cells", type=int, default=0,
+                    help="strong scaling: a region of this many cells split over the ranks (shard_range) instead of "
+                         "--cells per GPU")
+    ap.add_argument("--catchments", type=int, default=0,
+                    help="catchments of the whole region (default 100 per 1M-cell shard, 100 with --total-cells)")
+    ap.add_argument("--no-catchment-sums", action="store_true",
+                    help="skip the per-chunk catchment discharge sums (cell_statistics, RCCL allgather)")
+    ap.add_argument("--dump-sums", default="",
+                    help="rank 0 saves the region's catchment discharge sums [C][T] (.npy) after the timed steps")
+    ap.add_argument("--dist-check", action="store_true",
+                    help="launcher/rendezvous/collective rehearsal without the GPU: every rank combines "
+                         "catchment sums of a synthetic series over its shard, rank 0 checks them against "
+                         "the unsharded sums (tests/test_bench_launch.py)")
     ap.add_argument("--stack", choices=tuple(STACKS), default="pt_gs_k")
     ap.add_argument("--routing", action="store_true",
                     help="configs[4]: route avg_discharge through the synthetic river network (routing::uhg): "
@@ -128,20 +141,62 @@ BTK_DEFAULTS = [0.0025, 25.0, 0.5, 200000.0, 20.0]
 FP64_PEAK_FLOPS = 78.6e12        # MI355X FP64 matrix/vector peak (AMD spec sheet; not in MI355X_MICROARCH.md)
 
 
-def dist_setup(n_gpus):
+def launch_ranks(n_gpus):
+    """`bench.py --gpus N` started without a launcher: this parent process starts N fresh rank processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, 127.0.0.1 rendezvous) and exits
+    with the first failing rank's status. The parent never touches the GPU (no torch import), so no
+    process that initialised HIP is replaced; a rank that fails takes the others down instead of leaving
+    them blocked in a collective."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n_gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_gpus), LOCAL_WORLD_SIZE=str(n_gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dist_setup(n_gpus, use_gpu=True):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}: the line would not measure "
+                         f"{n_gpus} GPU(s)")
     pg = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        # one rank per GPU (RCCL over xGMI). SHYFT_DIST_BACKEND=gloo + more ranks than GPUs is only for
-        # rehearsing the multi-rank path on a one-GPU box; the device index wraps in that case.
-        n_dev = torch.cuda.device_count()
-        local = local % n_dev if n_dev else local
-        torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("SHYFT_DIST_BACKEND", "nccl"))
+        backend = os.environ.get("SHYFT_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+        if use_gpu:
+            # one rank per GPU (RCCL over xGMI). SHYFT_DIST_BACKEND=gloo + more ranks than GPUs is only for
+            # rehearsing the multi-rank path on a one-GPU box; the device index wraps in that case.
+            n_dev = torch.cuda.device_count()
+            if backend == "nccl" and n_dev < world:
+                raise SystemExit(f"bench.py: {world} ranks need {world} GPUs for RCCL, {n_dev} visible "
+                                 f"(SHYFT_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
+            local = local % n_dev if n_dev else local
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+        assert dist.get_world_size() == n_gpus
         pg = dist
     return world, rank, local, pg
 
@@ -157,9 +212,8 @@ def max_over_ranks(pg, local, v: float) -> float:
     if pg is None:
         return v
     import torch
-    t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local}")
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    from shyft_amd import distributed
+    return distributed.max_over_ranks(v, device=torch.device("cuda", local))
 
 
 def stack_defaults(stack, cells):
@@ -175,12 +229,31 @@ def stack_defaults(stack, cells):
     return synthetic.default_ptgsk_parameters(), synthetic.default_ptgsk_state(cells)
 
 
-def build_region(stack, cells, world, rank, local, chunk, n_steps_axis):
+class Layout:
+    """This rank's cells of the synthetic region: [off, off + n) of `total` cells, `n_catch` catchments in all.
+    Weak scaling (default): every rank owns --cells cells, 100 catchments per shard. Strong scaling
+    (--total-cells): the region is split by distributed.shard_range."""
+
+    def __init__(self, a, world, rank):
+        from shyft_amd import distributed
+        if a.total_cells:
+            b, e = distributed.shard_range(a.total_cells, world, rank)
+            self.off, self.n, self.total = b, e - b, a.total_cells
+            self.n_catch = a.catchments or 100
+            self.scaling = "strong"
+        else:
+            self.n = a.cells or (1 << 19 if a.stack == "hbv_stack" else 1 << 20)
+            self.off, self.total = rank * self.n, world * self.n
+            self.n_catch = a.catchments or 100 * world
+            self.scaling = "weak"
+
+
+def build_region(stack, L, local, chunk, n_steps_axis):
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K, PT_HPS_K, COLLECT_DISCHARGE
     sid = {"pt_gs_k": PT_GS_K, "hbv_stack": HBV_STACK, "pt_ss_k": PT_SS_K, "pt_hs_k": PT_HS_K, "pt_hps_k": PT_HPS_K}[stack]
-    r = HipRegion(sid, cells, device=local)
-    r.set_geo(synthetic.geo11(cells, n_catchments=100 * world, cell_offset=rank * cells, n_total=world * cells))
+    r = HipRegion(sid, L.n, device=local)
+    r.set_geo(synthetic.geo11(L.n, n_catchments=L.n_catch, cell_offset=L.off, n_total=L.total))
     r.set_parameters(stack_defaults(stack, 1)[0])
     r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, n_steps_axis, chunk)
     r.set_collection(COLLECT_DISCHARGE)
@@ -193,11 +266,11 @@ class Router:
     the partials are all-gathered and added in rank order (RCCL over xGMI); after the last chunk every rank
     convolves the network on its device (shyft_hip_route)."""
 
-    def __init__(self, r, cells, world, rank, local, n_axis, pg):
+    def __init__(self, r, L, local, n_axis, pg):
         import torch
         from shyft_amd import api, synthetic
-        self.n_catch = 100 * world
-        _, _, group = synthetic.cell_routing(cells, self.n_catch, cell_offset=rank * cells, n_total=world * cells)
+        self.n_catch = L.n_catch
+        _, _, group = synthetic.cell_routing(L.n, self.n_catch, cell_offset=L.off, n_total=L.total)
         self.G = self.n_catch * len(synthetic.ROUTE_DISTANCES)
         r.set_routing_groups(group, self.G)
         self.group = group
@@ -236,8 +309,36 @@ class Router:
         return self.out
 
 
-def run_year(r, cells, rank, chunk, k_steps, seed, stations=None, router=None, btk=False, btk_ms=None,
-             r_alt=None):
+class CatchmentSums:
+    """Per-chunk catchment discharge sums of the whole region (cell_statistics::sum_catchment_feature over
+    avg_discharge, core/cell_model.h:308-333; region_model::catchment_discharges, core/region_model.h:873-885):
+    each rank reduces its cells per catchment on its GPU (shyft_hip_catchment_sums, deterministic segment
+    sums), places the rows at their global catchment positions, and the partials are all-gathered (RCCL over
+    xGMI) and added in rank order (distributed.combine_partials) into [C][T] on every rank."""
+
+    def __init__(self, r, L, local, n_axis):
+        import torch
+        self.dev = torch.device("cuda", local)
+        self.C = L.n_catch
+        local_cids = [int(c) for c in r.catchment_ids()]
+        self.rows = torch.tensor([c - 1 for c in local_cids], dtype=torch.long, device=self.dev)  # cid = 1 + index
+        self.sums = torch.zeros((self.C, n_axis), dtype=torch.float64, device=self.dev)
+        self.part = None
+        self.full = None
+
+    def chunk(self, r, step0, n):
+        import torch
+        from shyft_amd import distributed
+        if self.part is None or self.part.shape[1] != n:
+            self.part = torch.empty((len(self.rows), n), dtype=torch.float64, device=self.dev)
+            self.full = torch.zeros((self.C, n), dtype=torch.float64, device=self.dev)
+        r.catchment_sums_device(0, step0, n, self.part.data_ptr())   # synchronous on the region's stream
+        self.full.index_copy_(0, self.rows, self.part)
+        distributed.combine_partials(self.full, out=self.sums[:, step0:step0 + n])
+
+
+def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, btk_ms=None,
+             r_alt=None, sums=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
     or IDW / BTK from the station network), then run_cells (and the routing group sums).
 
@@ -246,7 +347,7 @@ def run_year(r, cells, rank, chunk, k_steps, seed, stations=None, router=None, b
     chunk s runs, and the state is handed over device to device (shyft_hip_copy_state) before chunk s+1 runs.
     Every chunk's forcing is still produced inside the timed region; the generator just no longer adds to it."""
     if r_alt is not None and stations is None:
-        return _run_year_pipelined((r, r_alt), cells, rank, chunk, k_steps, seed, router)
+        return _run_year_pipelined((r, r_alt), L, chunk, k_steps, seed, router, sums)
     kernel_ms = []
     for s in range(k_steps):
         step0 = s * chunk
@@ -254,7 +355,7 @@ def run_year(r, cells, rank, chunk, k_steps, seed, stations=None, router=None, b
         # window, so the window moves without the NaN pre-fill of set_window
         r.move_window(step0, 0)
         if stations is None:
-            r.synthetic_forcing(seed, step0, chunk, cell_offset=rank * cells)
+            r.synthetic_forcing(seed, step0, chunk, cell_offset=L.off)
         else:
             xyz, vals = stations
             v = vals[s % len(vals)]
@@ -268,6 +369,8 @@ def run_year(r, cells, rank, chunk, k_steps, seed, stations=None, router=None, b
                     r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
         r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
+        if sums is not None:
+            sums.chunk(r, step0, chunk)
         if router is not None:
             router.chunk(r, step0, chunk)
     if router is not None:
@@ -275,10 +378,10 @@ def run_year(r, cells, rank, chunk, k_steps, seed, stations=None, router=None, b
     return kernel_ms
 
 
-def _run_year_pipelined(regs, cells, rank, chunk, k_steps, seed, router):
+def _run_year_pipelined(regs, L, chunk, k_steps, seed, router, sums):
     kernel_ms = []
     regs[0].move_window(0, 0)
-    regs[0].synthetic_forcing(seed, 0, chunk, cell_offset=rank * cells)
+    regs[0].synthetic_forcing(seed, 0, chunk, cell_offset=L.off)
     for s in range(k_steps):
         cur, nxt = regs[s % 2], regs[(s + 1) % 2]
         step0 = s * chunk
@@ -286,11 +389,13 @@ def _run_year_pipelined(regs, cells, rank, chunk, k_steps, seed, router):
         if s + 1 < k_steps:
             # host-synchronous on nxt's stream only: the generator overlaps cur's kernel
             nxt.move_window(step0 + chunk, 0)
-            nxt.synthetic_forcing(seed, step0 + chunk, chunk, cell_offset=rank * cells)
+            nxt.synthetic_forcing(seed, step0 + chunk, chunk, cell_offset=L.off)
         cur.synchronize()   # error check of the run (region_model::run_cells semantics)
         kernel_ms.append(cur.last_run_ms())
         if s + 1 < k_steps:
             nxt.copy_state_from(cur)
+        if sums is not None:
+            sums.chunk(cur, step0, chunk)
         if router is not None:
             router.chunk(cur, step0, chunk)
     if router is not None:
@@ -334,16 +439,23 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
-def pmc_summary(stack, cells, chunk):
-    """The committed rocprofv3 PMC summary of the dominant kernel (profiles/r01/<stack>_pmc.json, written by
-    tools/gpu_profile.sh + tools/pmc_summary.py) when it was taken on this exact workload; None otherwise. PMC
-    counters cannot be read from inside this process."""
-    path = os.path.join(ROOT, "profiles", "r01", f"{stack.replace('_', '')}_pmc.json")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+
+
+def workload_tag(a, cells):
+    """Key of a workload for the committed PMC summaries: they are only used for the exact same run."""
+    return (f"{a.stack}{'_idw' if a.idw else ''}{'_btk' if a.btk else ''}_c{cells}_k{a.chunk}"
+            f"_s{a.steps}_w{a.warmup}")
+
+
+def pmc_summary(a, cells):
+    """The committed rocprofv3 PMC summary of the dominant kernel (profiles/r02/pmc_<workload>.json, written by
+    tools/gpu_profile.sh + tools/pmc_summary.py from this same bench command) or None. PMC counters cannot be
+    read from inside this process."""
+    path = os.path.join(PROFILE_DIR, f"pmc_{workload_tag(a, cells)}.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
-        return None
-    if d.get("cells") != cells or d.get("chunk") != chunk:
         return None
     return d
 
@@ -358,16 +470,48 @@ def _cpu_model():
     return "unknown"
 
 
+def dist_check(a, world, rank, pg):
+    """--dist-check: the bench's launcher, rendezvous and catchment-sum combination without HIP. Each rank
+    sums a synthetic per-cell series (the generator's temperature of its shard) per catchment, the partials
+    go through distributed.combine_partials in rank order, and rank 0 compares with the unsharded sums."""
+    import torch
+    from shyft_amd import distributed, synthetic
+    L = Layout(a, world, rank)
+    T = 48
+    def sums_of(off, n):
+        cid = synthetic.geo11(n, n_catchments=L.n_catch, cell_offset=off, n_total=L.total)[:, 4].astype(np.int64)
+        f = synthetic.forcing(n, 0, T, synthetic.SEED, cell_offset=off)[0]            # [T][n]
+        out = np.zeros((L.n_catch, T))
+        for c in np.unique(cid):
+            out[c - 1] = f[:, cid == c].sum(axis=1)
+        return out
+    total = distributed.combine_partials(torch.from_numpy(sums_of(L.off, L.n))).numpy()
+    wall = distributed.max_over_ranks(float(rank + 1))
+    if rank == 0:
+        ref = sums_of(0, L.total)
+        print(json.dumps({"dist_check": True, "n_gpus": world, "backend": pg.get_backend() if pg else None,
+                          "cells": L.total, "catchments": L.n_catch, "max_over_ranks": wall,
+                          "max_abs_diff": float(np.abs(total - ref).max()),
+                          "checksum": float(total.sum())}), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
 def main():
     a = parse()
-    world, rank, local, pg = dist_setup(a.gpus)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+    world, rank, local, pg = dist_setup(a.gpus, use_gpu=not a.dist_check)
+    if a.dist_check:
+        return dist_check(a, world, rank, pg)
     import torch  # noqa: F401  (device init / sync)
     from shyft_amd import synthetic
 
-    cells = a.cells or (1 << 19 if a.stack == "hbv_stack" else 1 << 20)
+    L = Layout(a, world, rank)
+    cells = L.n
     chunk = a.chunk
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
-    r = build_region(a.stack, cells, world, rank, local, chunk, n_axis)
+    r = build_region(a.stack, L, local, chunk, n_axis)
     state0 = stack_defaults(a.stack, cells)[1]
     read_b, write_b, state_b, kernel_name = STACKS[a.stack]
     stations = None
@@ -376,37 +520,38 @@ def main():
     if a.idw:
         # station series prepared on the host before timing (the reference's region_env input);
         # each step uploads its chunk (14.6 MB) and interpolates 5 variables on the GPU
-        xyz = station_network(world * cells)
+        xyz = station_network(L.total)
         stations = (xyz, [station_values(xyz, s * chunk, chunk) for s in range(max(a.steps, a.warmup))])
 
     routing = (a.routing or a.stack == "pt_ss_k") and not a.no_routing
-    router = Router(r, cells, world, rank, local, n_axis, pg) if routing else None
+    router = Router(r, L, local, n_axis, pg) if routing else None
+    sums = None if a.no_catchment_sums else CatchmentSums(r, L, local, n_axis)
     r_alt = None
     if not a.idw and a.pipeline:
-        r_alt = build_region(a.stack, cells, world, rank, local, chunk, n_axis)
+        r_alt = build_region(a.stack, L, local, chunk, n_axis)
         if router is not None:
             router.attach(r_alt)
 
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
         r.set_state(state0)
-        run_year(r, cells, rank, chunk, a.warmup, synthetic.SEED, stations, router, a.btk, r_alt=r_alt)
+        run_year(r, L, chunk, a.warmup, synthetic.SEED, stations, router, a.btk, r_alt=r_alt, sums=sums)
     r.set_state(state0)   # the initial state is an input: resident in HBM before the timed region
     barrier_sync(pg, local)
     t0 = time.perf_counter()
     btk_ms = []
-    kernel_ms = run_year(r, cells, rank, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
-                         r_alt=r_alt)
+    kernel_ms = run_year(r, L, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
+                         r_alt=r_alt, sums=sums)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
     avg_kernel_ms = max_over_ranks(pg, local, float(np.mean(kernel_ms)))
 
-    total_cell_steps = world * cells * chunk * a.steps
+    total_cell_steps = L.total * chunk * a.steps
     value = total_cell_steps / wall
     bytes_per_launch = cells * chunk * (read_b + write_b) + cells * state_b
     achieved = bytes_per_launch / (avg_kernel_ms * 1e-3)
-    pmc = pmc_summary(a.stack, cells, chunk)
+    pmc = pmc_summary(a, cells)
     traffic_b = None if pmc is None else pmc["traffic_bytes_per_launch"]
     out = {
         "metric": METRIC if a.stack == "pt_gs_k" else METRIC.replace("pt_gs_k", a.stack),
@@ -417,7 +562,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": L.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8d generator, seed 20251015; " +
@@ -431,16 +576,19 @@ def main():
                         f"({a.steps} chunks of {chunk}), discharge_collector, default "
                         f"{dict(hbv_stack='HbvParameter', pt_ss_k='PTSSKParameter', pt_hs_k='PTHSKParameter', pt_hps_k='PTHPSKParameter').get(a.stack, 'PTGSKParameter')}",
             "cells_per_gpu": cells,
-            "total_cells": world * cells,
+            "total_cells": L.total,
+            "catchments": L.n_catch,
             "steps_per_chunk": chunk,
             "forcing": ("IDW/BTK from stations, per chunk, before its run" if a.idw else
                         "device generator, per chunk, overlapped with the previous chunk's run (two regions, state "
                         "handed over device to device)" if r_alt is not None else
                         "device generator, per chunk, before its run"),
-            "parallelism": f"cells sharded over {world} GPU(s), no data-path collective",
+            "parallelism": f"cells sharded over {world} GPU(s), no data-path collective"
+                           + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered "
+                              "(RCCL) and added in rank order"),
         },
         "kernel_ms_per_step": avg_kernel_ms,
-        "kernel_cell_steps_per_s": world * cells * chunk / (avg_kernel_ms * 1e-3),
+        "kernel_cell_steps_per_s": L.total * chunk / (avg_kernel_ms * 1e-3),
         "roofline": {
             "bound": "hbm",
             "achieved": achieved / 1e9,
@@ -464,7 +612,7 @@ def main():
         flops = 2.0 * cells * (N_STATIONS + 3) * chunk
         out["btk"] = {
             "ms_per_chunk": ms,
-            "cell_steps_per_s": world * cells * chunk / (ms * 1e-3),
+            "cell_steps_per_s": L.total * chunk / (ms * 1e-3),
             "roofline": {"bound": "fp64", "achieved": flops / (ms * 1e-3) / 1e12, "peak": FP64_PEAK_FLOPS / 1e12,
                          "unit": "TFLOP/s", "frac": flops / (ms * 1e-3) / FP64_PEAK_FLOPS,
                          "write_GBps": cells * chunk * 8 / (ms * 1e-3) / 1e9,
@@ -491,6 +639,15 @@ def main():
                                       f"device after the last chunk)")
         out["routing"] = {"rivers": len(router.rivers), "groups": router.G,
                           "outlet_mean_m3s": float(o[0].mean()), "outlet_max_m3s": float(o[0].max())}
+    if sums is not None:
+        T = a.steps * chunk
+        tot = sums.sums[:, :T]
+        out["catchment_sums"] = {"catchments": sums.C, "series": "avg_discharge", "steps": T,
+                                 "checksum": float(tot.sum().item()),
+                                 "note": "per chunk: segment sums on each GPU, allgather + rank-order add (inside "
+                                         "the timed region)"}
+        if a.dump_sums and rank == 0:
+            np.save(a.dump_sums, tot.cpu().numpy())
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         out["cpu_baseline"] = cpu_baseline(a.stack, a.cpu_cells, threads)

@@ -916,7 +916,9 @@ class region_model {
         for (size_t i = 0; i < size(); ++i) {
             const auto& g = geo_[i];
             if (!valid_routing_id(g.routing.id)) continue;
-            if (!catchment_filter_.empty() && !catchment_filter_[cid_to_cix_.at(g.catchment_id())]) continue;
+            // every cell routed to the river counts, whatever the catchment calculation filter says:
+            // routing::model::local_inflow (routing.h:345-350) iterates all cells; a filtered-out cell
+            // contributes the response series it holds (the last run that included it), as in the reference
             rivers.check_rid(g.routing.id);  // routing::model::verify_cell_river_connections (routing.h:313-320)
             const auto& p = cell_parameter(i);
             const double velocity = p[Stack::k_routing], alpha = p[Stack::k_routing + 1], beta = p[Stack::k_routing + 2];

@@ -107,6 +107,7 @@ struct shyft_hip_region {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_copy = nullptr;  // shyft_hip_copy_state: the copy out of this region's state has finished
     std::string err;
     double last_ms = 0.0;
 
@@ -470,6 +471,7 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
         hip_check(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
         hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
         hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
+        hip_check(hipEventCreateWithFlags(&h->ev_copy, hipEventDisableTiming), "hipEventCreate");
         h->d_state.alloc(h->n_state_fields() * n_cells);
         h->d_err.alloc(n_cells);
         h->d_flag.alloc(1);
@@ -489,6 +491,7 @@ void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -700,6 +703,11 @@ int shyft_hip_copy_state(shyft_hip_region* dst, const shyft_hip_region* src) {
         hip_check(hipStreamSynchronize(src->stream), "copy_state: source stream");
         hip_check(hipMemcpyAsync(dst->d_state.p, src->d_state.p, dst->n_state_fields() * dst->n * sizeof(double),
                                  hipMemcpyDeviceToDevice, dst->stream), "copy_state");
+        // anything later queued on the source stream (a run, set_state's upload) must not overwrite the source
+        // state while the destination stream still reads it
+        shyft_hip_region* s = const_cast<shyft_hip_region*>(src);
+        hip_check(hipEventRecord(s->ev_copy, dst->stream), "copy_state: record");
+        hip_check(hipStreamWaitEvent(s->stream, s->ev_copy, 0), "copy_state: order source stream");
         dst->has_state = true;
     });
 }
@@ -1107,21 +1115,26 @@ static void finish_run(shyft_hip_region* h) {
                              std::to_string(i) + ")");
 }
 
+// argument checks of region_model::run_cells (region_model.h:579-592), shared by the synchronous and the
+// asynchronous entry
+static void check_run_args(const shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {
+    const size_t ncore = 4096;  // the GPU path accepts any use_ncore the reference would
+    if (use_ncore > 100 * ncore)
+        throw std::runtime_error("illegal parameter value: use_ncore(" + std::to_string(use_ncore) +
+                                 " is more than 100 time available physical cores: " + std::to_string(ncore));
+    if (!(h->T > 0)) throw std::runtime_error("region_model::run with invalid time_axis invoked");
+    if (start_step < 0 || size_t(start_step + 1) > h->T)
+        throw std::runtime_error("region_model::run start_step must in range[0..n_steps-1>");
+    if (n_steps < 0) throw std::runtime_error("region_model::run n_steps must be range[0..time-axis-steps]");
+    if (size_t(start_step + n_steps) > h->T)
+        throw std::runtime_error("region_model::run start_step+n_steps must be within time-axis range");
+    if (!h->has_state) throw std::runtime_error("region_model::run: no state set");
+}
+
 int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {
     if (!h) return fail(h, "shyft_hip_run_cells: null handle");
     return guarded(h, [&] {
-        // argument checks of region_model::run_cells (region_model.h:579-592)
-        const size_t ncore = 4096;  // the GPU path accepts any use_ncore the reference would
-        if (use_ncore > 100 * ncore)
-            throw std::runtime_error("illegal parameter value: use_ncore(" + std::to_string(use_ncore) +
-                                     " is more than 100 time available physical cores: " + std::to_string(ncore));
-        if (!(h->T > 0)) throw std::runtime_error("region_model::run with invalid time_axis invoked");
-        if (start_step < 0 || size_t(start_step + 1) > h->T)
-            throw std::runtime_error("region_model::run start_step must in range[0..n_steps-1>");
-        if (n_steps < 0) throw std::runtime_error("region_model::run n_steps must be range[0..time-axis-steps]");
-        if (size_t(start_step + n_steps) > h->T)
-            throw std::runtime_error("region_model::run start_step+n_steps must be within time-axis range");
-        if (!h->has_state) throw std::runtime_error("region_model::run: no state set");
+        check_run_args(h, use_ncore, start_step, n_steps);
         launch_run(h, start_step, n_steps);
         finish_run(h);
     });
@@ -1129,7 +1142,10 @@ int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, i
 
 int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps) {
     if (!h) return fail(h, "shyft_hip_run_cells_async: null handle");
-    return guarded(h, [&] { launch_run(h, start_step, n_steps); });
+    return guarded(h, [&] {
+        check_run_args(h, 0, start_step, n_steps);
+        launch_run(h, start_step, n_steps);
+    });
 }
 
 int shyft_hip_synchronize(shyft_hip_region* h) {

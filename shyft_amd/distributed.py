@@ -28,20 +28,37 @@ def env_rank() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def combine_partials(partial, group=None):
+def _wire(t, group=None):
+    """The tensor the backend can move: RCCL ("nccl") takes device tensors; gloo (the CPU rehearsal
+    backend, also used for more ranks than GPUs on one box) only host tensors."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        return t.cpu()
+    return t
+
+
+def combine_partials(partial, group=None, out=None):
     """Deterministic cross-rank sum of per-rank partials (a torch tensor, same shape on every
-    rank): all_gather, then add in rank order. Returns the total on every rank."""
+    rank): all_gather, then add in rank order. Returns the total on every rank (written into
+    `out` when given)."""
     import torch
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
-        return partial.clone()
+        if out is None:
+            return partial.clone()
+        out.copy_(partial)
+        return out
     world = dist.get_world_size(group)
-    parts = [torch.empty_like(partial) for _ in range(world)]
-    dist.all_gather(parts, partial.contiguous(), group=group)
+    wire = _wire(partial.contiguous(), group)
+    parts = [torch.empty_like(wire) for _ in range(world)]
+    dist.all_gather(parts, wire, group=group)
     total = parts[0].clone()
     for p in parts[1:]:
         total += p
-    return total
+    if out is None:
+        return total.to(partial.device)
+    out.copy_(total)
+    return out
 
 
 def max_over_ranks(value: float, device=None, group=None) -> float:
@@ -49,7 +66,7 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = _wire(torch.tensor([float(value)], dtype=torch.float64, device=device), group)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
 

@@ -178,6 +178,10 @@ class HipRegion:
         self._chk(self._L.shyft_hip_get_series(self.h, series, step0, n, _ptr(out), 0))
         return out
 
+    def get_series_device(self, series: int, step0: int, n: int, dev_ptr: int):
+        """[n][cells] rows of a collected series into device memory (e.g. a torch tensor's data_ptr())."""
+        self._chk(self._L.shyft_hip_get_series(self.h, series, step0, n, C.c_void_p(dev_ptr), 1))
+
     def get_state_series(self, field: int, step0: int, n: int) -> np.ndarray:
         out = np.empty((n, self.n), dtype=np.float64)
         self._chk(self._L.shyft_hip_get_state_series(self.h, field, step0, n, _ptr(out), 0))

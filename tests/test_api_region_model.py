@@ -298,3 +298,42 @@ def test_pt_ss_k_model_init_and_run():
                                       for i in range(n)], axis=1))
     r.run_cells()
     assert np.allclose(r.get_series(0, 0, 240).sum(axis=1), q, rtol=1e-13, atol=0)
+
+
+def test_routing_counts_filtered_out_cells():
+    """routing::model::local_inflow (routing.h:345-350) sums every cell routed to the river, whatever the
+    catchment calculation filter says: a filtered-out cell contributes the response it holds from the last
+    run that included it (its collector series are not touched by a run that skips it)."""
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k
+    n = 20
+    model = build_model(pt_gs_k.PTGSKModel, pt_gs_k.PTGSKParameter, n, num_catchments=2)
+    ta = api.TimeAxisFixedDeltaT(api.Calendar().time(2015, 1, 1, 0, 0, 0), api.deltahours(1), 48)
+    model.initialize_cell_environment(ta)
+    model.interpolate(interpolation_parameter(), dummy_env(ta, model.get_cells()[n // 2].geo.mid_point()))
+    s0 = pt_gs_k.PTGSKStateVector()
+    for _ in range(n):
+        si = pt_gs_k.PTGSKState()
+        si.kirchner.q = 40.0
+        s0.append(si)
+    model.set_states(s0)
+    model.run_cells()
+    all_cids = api.IntVector()
+    q_all = model.statistics.discharge(all_cids).values.to_numpy()
+    q2_first = model.statistics.discharge(api.IntVector([2])).values.to_numpy()
+    model.river_network.add(api.River(1, api.RoutingInfo(0, 0.0), api.UHGParameter(1 / 3.60, 7.0, 0.0)))
+    model.connect_catchment_to_river(1, 1)
+    model.connect_catchment_to_river(2, 1)
+    # second run of catchment 1 only, from a different state: catchment 2 keeps its first-run series
+    model.set_catchment_calculation_filter(api.IntVector([1]))
+    s1 = pt_gs_k.PTGSKStateVector()
+    for _ in range(n):
+        si = pt_gs_k.PTGSKState()
+        si.kirchner.q = 5.0
+        s1.append(si)
+    model.set_states(s1)
+    model.run_cells()
+    q1_second = model.statistics.discharge(api.IntVector([1])).values.to_numpy()
+    local = model.river_local_inflow_m3s(1).values.to_numpy()
+    assert not np.allclose(q1_second + q2_first, q_all)
+    assert np.allclose(local, q1_second + q2_first, rtol=1e-12, atol=1e-12)

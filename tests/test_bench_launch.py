@@ -1,0 +1,63 @@
+"""bench.py's multi-rank path (BASELINE configs[3]/[4] at N>1).
+
+`bench.py --gpus N` without an outside launcher starts N rank processes itself (a parent that never touches
+the GPU), every rank asserts WORLD_SIZE == N, and the per-chunk catchment discharge sums are all-gathered and
+added in rank order (distributed.combine_partials). CPU tests drive that launcher, rendezvous and collective
+with gloo (--dist-check); the GPU tests run the real sharded HipRegion bench with two ranks on one GPU
+(SHYFT_DIST_BACKEND=gloo) and compare the combined catchment sums with a single-rank run of the same region.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p, (json.loads(lines[-1]) if lines else None)
+
+
+@pytest.mark.parametrize("world,cells,catch", [(2, 10001, 37), (3, 4096, 100)])
+def test_launcher_gloo_dist_check(world, cells, catch):
+    p, out = _bench(["--gpus", str(world), "--dist-check", "--total-cells", str(cells), "--catchments", str(catch)])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["n_gpus"] == world and out["backend"] == "gloo"
+    assert out["max_over_ranks"] == float(world)
+    # rank-order sums of shard partials vs the unsharded sums (catchments split across ranks reassociate)
+    assert out["max_abs_diff"] < 1e-9
+
+
+def test_world_size_mismatch_fails():
+    p, out = _bench(["--gpus", "2", "--dist-check"], env_extra={"WORLD_SIZE": "3", "RANK": "0"})
+    assert p.returncode != 0 and out is None
+    assert "WORLD_SIZE=3" in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stack", ["pt_gs_k", "hbv_stack"])
+def test_two_ranks_one_gpu_catchment_sums_match_single_rank(stack, tmp_path):
+    """Two real ranks (gloo on one GPU) over a 4096-cell region == one rank over the same region: the shard
+    boundary (cell 2048) falls on a catchment boundary, so every catchment is summed by one rank and the
+    rank-order combination adds zeros; the sums must agree bit for bit."""
+    common = ["--stack", stack, "--total-cells", "4096", "--catchments", "100", "--chunk", "48", "--steps", "3",
+              "--warmup", "0", "--no-cpu-baseline", "--no-routing"]
+    p1, o1 = _bench(["--gpus", "1", "--dump-sums", str(tmp_path / "s1.npy")] + common)
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    p2, o2 = _bench(["--gpus", "2", "--dump-sums", str(tmp_path / "s2.npy")] + common,
+                    env_extra={"SHYFT_DIST_BACKEND": "gloo"})
+    assert p2.returncode == 0, p2.stderr[-2000:]
+    assert o1["n_gpus"] == 1 and o2["n_gpus"] == 2 and o2["scaling"] == "strong"
+    s1, s2 = np.load(tmp_path / "s1.npy"), np.load(tmp_path / "s2.npy")
+    assert s1.shape == (100, 144) and np.isfinite(s1).all() and s1.sum() > 0
+    assert np.array_equal(s1, s2)

@@ -1,0 +1,185 @@
+"""BASELINE configs[2] (C3) parity: inverse-distance interpolation from S = 500 stations, and the chained
+IDW -> pt_gs_k run, device against the oracle, bit for bit.
+
+The gather kernel stages station rows through LDS a tile at a time; at 500 stations the temperature tile holds
+5 rows (32 KB budget minus the station coordinates), so a 730-row chunk runs ~146 tiles with their barriers and
+per-tile finite-row flags. Above ~1365 sources a row set no longer fits and the kernel reads rows from global
+memory (lds_rows = 0); the reference's own 70 x 70 = 4900-source scenario
+(test/inverse_distance_test.cpp:396-450, "test_performance") covers that path.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from tests.test_idw import IDW_PARAMS, oracle_idw
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+HOUR = 3600 * 10**6
+
+
+def c3_region(n_cells, rows, step0=0, nan_frac=0.03, seed=11):
+    """The bench's C3 layout scaled to n_cells: synthetic grid cells, 500 stations on the 22 x 23 grid
+    covering the region (bench.station_network), station values from the device generator's host twin
+    (bench.station_values), plus missing observations in a random subset of the rows."""
+    import bench
+    from shyft_amd import synthetic
+    geo = synthetic.geo11(n_cells)
+    xyz = bench.station_network(n_cells)
+    vals = bench.station_values(xyz, step0, rows)                   # [5][rows][S]
+    rng = np.random.default_rng(seed)
+    bad_rows = rng.uniform(size=rows) < 0.2
+    miss = (rng.uniform(size=vals.shape) < nan_frac) & bad_rows[None, :, None]
+    vals = np.where(miss, np.nan, vals)
+    return geo, xyz, vals
+
+
+def _device_interpolate(geo, xyz, vals, var, prm, splits):
+    from shyft_amd import synthetic
+    from shyft_amd.region import HipRegion, PT_GS_K
+    T, N = vals.shape[0], geo.shape[0]
+    r = HipRegion(PT_GS_K, N)
+    try:
+        r.set_geo(geo)
+        r.set_parameters(synthetic.default_ptgsk_parameters())
+        r.set_time_axis(synthetic.T0_2015_US, HOUR, T)
+        b = 0
+        for e in list(splits) + [T]:
+            r.interpolate(var, xyz, vals[b:e], b, prm)
+            b = e
+        return r.get_forcing(var, 0, T)
+    finally:
+        r.close()
+
+
+def _same(got, exp):
+    same = (got == exp) | (np.isnan(got) & np.isnan(exp))
+    return same.all(), f"{(~same).sum()} of {same.size} differ; max abs {np.nanmax(np.abs(got - exp))}"
+
+
+C3_PARAMS = {   # bench.IDW_DEFAULTS (inverse_distance.h:38-74 defaults) per forcing variable
+    0: [20, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],
+    1: [20, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],
+    2: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],
+    3: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],
+    4: [10, 200000.0, 2.0, 1.0, -0.006, 0.0, 1.02],
+}
+
+
+def test_c3_station_network_shape():
+    """The test region is the bench's: 500 stations, values from the same generator, NaNs only where planted."""
+    geo, xyz, vals = c3_region(1500, 50)
+    assert xyz.shape == (500, 3) and vals.shape == (5, 50, 500)
+    assert xyz[:, 0].max() == pytest.approx(math.ceil(math.sqrt(1500)) * 1000.0)
+    assert np.isnan(vals).any() and np.isfinite(vals).mean() > 0.99
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("var,by_equation", [(0, False), (0, True), (1, False), (2, False), (3, False), (4, False)])
+def test_c3_idw_500_stations_730_rows_bitexact(var, by_equation):
+    """S = 500, 730 rows in one call plus a 2-call split (the neighbour table is reused): the multi-tile LDS
+    loop of the gather kernel against the oracle's run_interpolation (inverse_distance.h:142-250)."""
+    geo, xyz, vals = c3_region(1500, 730)
+    kind = IDW_PARAMS[var][0]
+    prm = list(C3_PARAMS[var])
+    prm[5] = 1.0 if by_equation else 0.0
+    v = np.ascontiguousarray(vals[var])
+    exp = oracle_idw(kind, xyz, v, geo[:, :3], prm, dst_slope=geo[:, 5])
+    assert np.isfinite(exp).all()   # 500 stations within 200 km: every cell always has a valid neighbour
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, []), exp)
+    assert ok, msg
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, [333]), exp)
+    assert ok, msg
+
+
+def reference_performance_scenario(n=72):
+    """inverse_distance_test.cpp:396-450: 70 x 70 temperature sources 3 km apart, z = (i + j) 500 / 140,
+    constant series 10 - 0.1 x/1000 - 0.6/100 z; 55 x 55 cells (mocks.h:417-427 GenerateTestGrid: x, y = 500 +
+    1000 i, z = 100 + (x + y) 700/110); Parameter(2 * 3000, 4): max_distance 6 km, 4 neighbours."""
+    s_n, s_dxy = 70, 3000.0
+    i, j = np.meshgrid(np.arange(s_n), np.arange(s_n), indexing="ij")
+    xyz = np.stack([s_dxy * i.ravel(), s_dxy * j.ravel(), (i + j).ravel() * 500.0 / (s_n + s_n)], 1)
+    v = 10.0 - xyz[:, 0] * 0.1 / 1000.0 - 0.6 / 100.0 * xyz[:, 2]
+    vals = np.tile(v, (n, 1))
+    nx = ny = 55
+    dz = (800.0 - 100.0) / (nx + ny)
+    cx, cy = np.meshgrid(np.arange(nx), np.arange(ny), indexing="ij")
+    geo = np.zeros((nx * ny, 11))
+    geo[:, 0] = 500.0 + cx.ravel() * 1000
+    geo[:, 1] = 500.0 + cy.ravel() * 1000
+    geo[:, 2] = 100.0 + (cx + cy).ravel() * dz
+    geo[:, 3] = 1e6
+    geo[:, 4] = 1
+    geo[:, 5] = 0.9
+    geo[:, 10] = 1.0
+    prm = [4, 2 * s_dxy, 2.0, 1.0, -0.006, 0.0, 1.02]
+    return geo, xyz, vals, prm
+
+
+def test_reference_4900_source_scenario_oracle():
+    """The oracle on the reference's performance scenario: finite everywhere (every cell has sources within
+    6 km), and the temperature stays inside the sources' range adjusted by the gradient."""
+    from tests.test_idw import TEMPERATURE
+    geo, xyz, vals, prm = reference_performance_scenario(8)
+    out = oracle_idw(TEMPERATURE, xyz, vals, geo[:, :3], prm)
+    assert np.isfinite(out).all()
+    assert np.all(out == out[0])           # constant source series -> constant cell series
+    assert -1.0 < out.min() and out.max() < 10.0   # 10 - 0.1 x/km over 55 km, -0.006 C/m over <= 800 m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_nan", [False, True])
+def test_reference_4900_source_scenario_bitexact(with_nan):
+    """4900 sources: 3 x 4900 x 8 B of coordinates exceed the 32 KB LDS budget, so the gather reads rows from
+    global memory (lds_rows = 0), the path no other test reaches."""
+    from tests.test_idw import TEMPERATURE
+    geo, xyz, vals, prm = reference_performance_scenario(72)
+    if with_nan:
+        rng = np.random.default_rng(3)
+        vals = np.where(rng.uniform(size=vals.shape) < 0.1, np.nan, vals)
+    exp = oracle_idw(TEMPERATURE, xyz, vals, geo[:, :3], prm)
+    ok, msg = _same(_device_interpolate(geo, xyz, vals, 0, prm, [30]), exp)
+    assert ok, msg
+
+
+@pytest.mark.gpu
+def test_c3_chain_idw_then_pt_gs_k_bitexact():
+    """run_interpolation (all five variables by IDW from the 500 stations, use_idw_for_temperature) followed by
+    run_cells, against the same chain on the oracle: region_model::interpolate (region_model.h:397-555) feeding
+    cell::run (pt_gs_k_cell_model.h:243-262)."""
+    from shyft_amd import synthetic
+    from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_ALL
+    from tests import oracle_lib
+    N, T = 1500, 730
+    geo, xyz, vals = c3_region(N, T, nan_frac=0.01)
+    f = np.empty((5, T, N))
+    for var in range(5):
+        f[var] = oracle_idw(IDW_PARAMS[var][0], xyz, np.ascontiguousarray(vals[var]), geo[:, :3], C3_PARAMS[var],
+                            dst_slope=geo[:, 5])
+    p = synthetic.default_ptgsk_parameters()
+    s = synthetic.default_ptgsk_state(N)
+    exp = oracle_lib.ptgsk_run(geo, p, s, synthetic.T0_2015_US, HOUR, f, full=True)
+    r = HipRegion(PT_GS_K, N)
+    try:
+        r.set_geo(geo)
+        r.set_parameters(p)
+        r.set_time_axis(synthetic.T0_2015_US, HOUR, T)
+        r.set_collection(COLLECT_ALL)
+        r.set_state(s)
+        for var in range(5):
+            r.interpolate(var, xyz, np.ascontiguousarray(vals[var]), 0, C3_PARAMS[var])
+        got_f = np.stack([r.get_forcing(v, 0, T) for v in range(5)])
+        r.run_cells(0, 0, T)
+        got = np.stack([r.get_series(k, 0, T) for k in range(8)])
+        st = r.get_state()
+    finally:
+        r.close()
+    ok, msg = _same(got_f, f)
+    assert ok, "forcing: " + msg
+    ok, msg = _same(got, exp["full"])
+    assert ok, "series: " + msg
+    assert np.array_equal(st, exp["state"])
