@@ -201,6 +201,13 @@ def dist_setup(n_gpus, use_gpu=True):
     return world, rank, local, pg
 
 
+def _backend_name(pg):
+    if pg is None:
+        return "single rank"
+    b = pg.get_backend()
+    return "RCCL" if b == "nccl" else b
+
+
 def barrier_sync(pg, local):
     import torch
     if pg is not None:
@@ -585,7 +592,7 @@ def main():
                         "device generator, per chunk, before its run"),
             "parallelism": f"cells sharded over {world} GPU(s), no data-path collective"
                            + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered "
-                              "(RCCL) and added in rank order"),
+                              f"({_backend_name(pg)}) and added in rank order"),
         },
         "kernel_ms_per_step": avg_kernel_ms,
         "kernel_cell_steps_per_s": L.total * chunk / (avg_kernel_ms * 1e-3),

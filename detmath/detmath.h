@@ -26,10 +26,21 @@
 #include <hip/hip_runtime.h>
 #define DM_FN __host__ __device__ inline
 #define DM_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#define DM_FABS(a) __builtin_fabs(a)
 #else
 #include <cmath>
 #define DM_FN inline
 #define DM_FMA(a, b, c) std::fma((a), (b), (c))
+#define DM_FABS(a) std::fabs(a)
+#endif
+
+// DM_NO_SPECULATE(): marks a rarely taken branch (the incomplete gamma's 2^-200 rescaling) as a real branch.
+// Without it the gfx950 compiler if-converts the rescale into every unrolled series iteration (three ldexp
+// and six selects per term, more than the term itself); as a branch it costs one scalar exec test.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DM_NO_SPECULATE() asm volatile("")
+#else
+#define DM_NO_SPECULATE() ((void)0)
 #endif
 
 #if defined(__clang__)
@@ -37,6 +48,7 @@
 #endif
 
 namespace detmath {
+
 
 DM_FN uint64_t as_u64(double x) {
     uint64_t u;
@@ -297,55 +309,64 @@ struct dm_policy {
     DM_FN static double log(double x) { return detmath::log(x); }
 };
 
+// The evaluation in pieces: gamma_pq_kind picks the special case or the method, gamma_pq_prefix is the
+// prefix, gamma_series_sums / gamma_cf_terms run the series / continued fraction, gamma_pq_finish combines.
+// gamma_pq below is exactly their composition (the prefix, series and continued-fraction chains of one
+// evaluation are independent until the finish, so a caller may also run them apart).
+enum { GPQ_NAN = 0, GPQ_ZERO = 1, GPQ_INF = 2, GPQ_SERIES = 3, GPQ_CF = 4 };
+
+DM_FN int gamma_pq_kind(double a, double x) {
+    if (is_nan(a) || is_nan(x)) return GPQ_NAN;
+    if (x <= 0.0) return GPQ_ZERO;
+    if (x == inf()) return GPQ_INF;
+    return x < a + 1.0 ? GPQ_SERIES : GPQ_CF;
+}
+
 template <class M>
-DM_FN gamma_pq_result gamma_pq(double a, double x, double lga, double eps = 2.220446049250313e-16) {
+DM_FN double gamma_pq_prefix(double a, double x, double lga) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
-    gamma_pq_result r;
-    if (is_nan(a) || is_nan(x)) {
-        r.p = r.p1 = r.prefix = qnan();
-        return r;
-    }
-    if (x <= 0.0) {
-        r.p = r.p1 = r.prefix = 0.0;
-        return r;
-    }
-    if (x == inf()) {
-        r.p = r.p1 = 1.0;
-        r.prefix = 0.0;
-        return r;
-    }
-    const double prefix = M::exp(a * M::log(x) - x - lga);
-    r.prefix = prefix;
-    const double SCALE_HI = 1.0e200, SCALE = 6.2230152778611417e-61;  // 2^-200
-    if (x < a + 1.0) {
-        double ap = a, E = 1.0, B = 0.0, xn = 1.0;
-        for (int n = 1; n <= 2000; ++n) {
-            ap = ap + 1.0;
-            xn = xn * x;
-            E = E * ap;
-            B = DM_FMA(B, ap, xn);
-            if (xn < eps * (B + E)) break;
-            if (E > SCALE_HI) {
-                E = E * SCALE;
-                B = B * SCALE;
-                xn = xn * SCALE;
-            }
+    return M::exp(a * M::log(x) - x - lga);
+}
+
+constexpr double GPQ_SCALE_HI = 1.0e200, GPQ_SCALE = 6.2230152778611417e-61;  // 2^-200
+
+// series: E = (a+1)...(a+n), B = sum_{k>=1} x^k E/(a+1..a+k)
+DM_FN void gamma_series_sums(double a, double x, double eps, double& B_out, double& E_out) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    double ap = a, E = 1.0, B = 0.0, xn = 1.0;
+    for (int n = 1; n <= 2000; ++n) {
+        ap = ap + 1.0;
+        xn = xn * x;
+        E = E * ap;
+        B = DM_FMA(B, ap, xn);
+        if (xn < eps * (B + E)) break;
+        if (E > GPQ_SCALE_HI) {
+            DM_NO_SPECULATE();
+            E = E * GPQ_SCALE;
+            B = B * GPQ_SCALE;
+            xn = xn * GPQ_SCALE;
         }
-        const double aE = a * E;
-        const double p = prefix * ((B + E) / aE);
-        const double p1 = prefix * (B / aE);
-        r.p = p < 1.0 ? p : 1.0;
-        r.p1 = p1 < 1.0 ? p1 : 1.0;
-        return r;
     }
-    // Wallis recurrence for K = b0 + a1/(b1 + a2/(b2 + ...)); Q = prefix / K
+    B_out = B;
+    E_out = E;
+}
+
+// Wallis recurrence for K = b0 + a1/(b1 + a2/(b2 + ...)) = P / Qd
+DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double& Qd_out) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
     double b = x + 1.0 - a;
     double Pm = 1.0, Qm = 0.0;  // n-1
     double P = b, Qd = 1.0;     // n (= 0)
+    double di = 0.0;  // i as a double (exact), counted instead of converted each term
     for (int i = 1; i <= 2000; ++i) {
-        const double an = -i * (i - a);
+        di = di + 1.0;
+        const double an = -di * (di - a);
         b = b + 2.0;
         const double Pn = DM_FMA(b, P, an * Pm);
         const double Qn = DM_FMA(b, Qd, an * Qm);
@@ -354,19 +375,58 @@ DM_FN gamma_pq_result gamma_pq(double a, double x, double lga, double eps = 2.22
         const double diff = cross - P * Qn;
         Pm = P; Qm = Qd;
         P = Pn; Qd = Qn;
-        if ((diff < 0 ? -diff : diff) <= eps * (cross < 0 ? -cross : cross)) break;
-        const double aP = P < 0 ? -P : P;
-        if (aP > SCALE_HI) {
-            P = P * SCALE; Qd = Qd * SCALE; Pm = Pm * SCALE; Qm = Qm * SCALE;
+        if (DM_FABS(diff) <= eps * DM_FABS(cross)) break;
+        const double aP = DM_FABS(P);
+        if (aP > GPQ_SCALE_HI) {
+            DM_NO_SPECULATE();
+            P = P * GPQ_SCALE; Qd = Qd * GPQ_SCALE; Pm = Pm * GPQ_SCALE; Qm = Qm * GPQ_SCALE;
         }
     }
-    const double q = prefix * (Qd / P);
-    const double q1 = q + prefix / a;
-    const double p = 1.0 - q;
-    const double p1 = 1.0 - q1;
-    r.p = p > 0.0 ? p : 0.0;
-    r.p1 = p1 > 0.0 ? p1 : 0.0;
+    P_out = P;
+    Qd_out = Qd;
+}
+
+// kind from gamma_pq_kind; prefix from gamma_pq_prefix (SERIES / CF); (u, v) = (B, E) or (P, Qd)
+DM_FN gamma_pq_result gamma_pq_finish(int kind, double a, double prefix, double u, double v) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    gamma_pq_result r;
+    if (kind == GPQ_NAN) {
+        r.p = r.p1 = r.prefix = qnan();
+    } else if (kind == GPQ_ZERO) {
+        r.p = r.p1 = r.prefix = 0.0;
+    } else if (kind == GPQ_INF) {
+        r.p = r.p1 = 1.0;
+        r.prefix = 0.0;
+    } else if (kind == GPQ_SERIES) {
+        r.prefix = prefix;
+        const double aE = a * v;
+        const double p = prefix * ((u + v) / aE);
+        const double p1 = prefix * (u / aE);
+        r.p = p < 1.0 ? p : 1.0;
+        r.p1 = p1 < 1.0 ? p1 : 1.0;
+    } else {
+        r.prefix = prefix;
+        const double q = prefix * (v / u);
+        const double q1 = q + prefix / a;
+        const double p = 1.0 - q;
+        const double p1 = 1.0 - q1;
+        r.p = p > 0.0 ? p : 0.0;
+        r.p1 = p1 > 0.0 ? p1 : 0.0;
+    }
     return r;
+}
+
+template <class M>
+DM_FN gamma_pq_result gamma_pq(double a, double x, double lga, double eps = 2.220446049250313e-16) {
+    const int kind = gamma_pq_kind(a, x);
+    if (kind < GPQ_SERIES) return gamma_pq_finish(kind, a, 0.0, 0.0, 0.0);
+    const double prefix = gamma_pq_prefix<M>(a, x, lga);
+    double u, v;
+    if (kind == GPQ_SERIES) gamma_series_sums(a, x, eps, u, v);
+    else gamma_cf_terms(a, x, eps, u, v);
+    return gamma_pq_finish(kind, a, prefix, u, v);
 }
 
 DM_FN double gamma_p(double a, double x) { return gamma_pq<dm_policy>(a, x, detmath::lgamma(a)).p; }

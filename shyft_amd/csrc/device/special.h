@@ -23,7 +23,7 @@ __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b 
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
 // inlining policy of the heavy device functions (tuned for VGPR pressure / I-cache)
 #ifndef SHYFT_INL_SNOW
-#define SHYFT_INL_SNOW __noinline__
+#define SHYFT_INL_SNOW inline
 #endif
 #ifndef SHYFT_INL_GS
 #define SHYFT_INL_GS inline

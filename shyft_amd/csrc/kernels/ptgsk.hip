@@ -22,6 +22,23 @@
 
 using namespace shyft_dev;
 
+#ifdef SHYFT_PROF
+// phase timing (profiling builds only): per-wavefront s_memtime deltas summed over the launch
+__device__ unsigned long long g_ptgsk_prof[8];
+extern "C" int shyft_ptgsk_prof_read(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptgsk_prof), sizeof(g_ptgsk_prof)) != hipSuccess) return 1;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ptgsk_prof), z, sizeof z) != hipSuccess;
+}
+#define PROF_DECL unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long prof_t = __builtin_amdgcn_s_memtime();
+#define PROF_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[k] += t_ - prof_t; prof_t = t_; } while (0)
+#define PROF_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 6; ++k_) atomicAdd(&g_ptgsk_prof[k_], prof_acc[k_]); } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(k) ((void)0)
+#define PROF_FLUSH() ((void)0)
+#endif
+
 namespace {
 
 #ifndef SHYFT_BLOCK
@@ -64,11 +81,6 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     const double cell_area_m2 = cc[PC_AREA * N + lc];
     const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
 
-    const double gm_direct = P[PK_GM_DIRECT];
-    const double gm_routed = 1 - gm_direct;
-    const double dtf = P[PK_DTF];
-    const double p_corr = P[PK_PCORR];
-    const double kc1 = P[PK_C1], kc2 = P[PK_C2], kc3 = P[PK_C3];
     const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
 
     // state -> registers
@@ -122,7 +134,13 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     };
 
     const int i_end = a.step0 + a.n_steps;
+    PROF_DECL
     for (int i = a.step0; i < i_end; ++i) {
+        const double gm_direct = P[PK_GM_DIRECT];
+        const double gm_routed = 1 - gm_direct;
+        const double dtf = P[PK_DTF];
+        const double p_corr = P[PK_PCORR];
+        const double kc1 = P[PK_C1], kc2 = P[PK_C2], kc3 = P[PK_C3];
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + lc;
         const size_t ff = ENS ? wi * NF + fcl : fo;
@@ -144,6 +162,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
         m.done = true;
         if (valid)
             gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc);
+        PROF_MARK(0);  // forcing + gs_front
         double z = 0.0;
         if (COMPACT) {
             if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (race-free: see DESIGN.md)
@@ -153,24 +172,21 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
                 jz1[slot] = m.z1; ja1[slot] = m.a1; jb1[slot] = m.b1; ja2[slot] = m.a2; jb2[slot] = m.b2;
             }
             __syncthreads();
+            PROF_MARK(1);  // job queue + barrier
             const int nj = jcount[i & 1];
             if (nj > 0) {
-#ifdef SHYFT_ROTATE
-                // rotate which wavefront starts the queue so the Brent load spreads over the SIMDs
-                const int t = (threadIdx.x + BLOCK - 64 * (i % (BLOCK / 64))) % BLOCK;
-#else
-                const int t = threadIdx.x;
-#endif
-                for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j]);
+                for (int j = threadIdx.x; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j]);
                 __syncthreads();
                 if (slot >= 0) z = jres[slot];
             }
         } else if (m.need) {
             z = gs_solve_lwc(m);
         }
+        PROF_MARK(2);  // Brent phase
         if (!valid) continue;
         double gs_sca, gs_storage, gs_outflow;
         gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc);
+        PROF_MARK(3);  // gs_back
 
         // glacier_melt::step (glacier_melt.h:47-52)
         const double sca_area = cell_area_m2 * gs_sca;
@@ -203,7 +219,9 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
             R[7 * RS + fo] = pot_evap;
         }
         if (SS && i + 1 == i_end) collect_state(wi + 1);
+        PROF_MARK(4);  // glacier, PT, AE, kirchner, outputs
     }
+    PROF_FLUSH();
     if (!valid) return;
     st[PS_ALBEDO * N + cell] = s.albedo;
     st[PS_LWC * N + cell] = s.lwc;
