@@ -56,7 +56,7 @@ STACKS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=12)
@@ -95,7 +95,7 @@ def parse():
     ap.add_argument("--btk", action="store_true",
                     help="as --idw, but temperature by Bayesian kriging from the stations (the reference's default "
                          "temperature method, region_model.h:460-468)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # configs[2] station network: 500 stations on a 22 x 23 grid at 45 km spacing
@@ -604,8 +604,12 @@ def main():
             "frac": achieved / HBM_PEAK_BPS,
             "traffic": None if traffic_b is None else traffic_b / (avg_kernel_ms * 1e-3) / 1e9,
             "traffic_bytes_per_launch": traffic_b,
-            "traffic_source": "rocprofv3 FETCH_SIZE + WRITE_SIZE per launch, mean over the 12 chunks of a year "
-                              "(profiles/r01/*_pmc.json), over this run's average launch duration, GB/s like achieved",
+            "traffic_source": (None if pmc is None else
+                               f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json: rocprofv3 "
+                               f"FETCH_SIZE x {pmc['calibration']['fetch_correction']:.3f} + WRITE_SIZE x "
+                               f"{pmc['calibration']['write_correction']:.3f} (gfx950 correction calibrated in the same "
+                               "run, tools/pmc_summary.py), mean over the timed launches of this same command, over "
+                               "this run's mean launch duration"),
             "kernel": kernel_name,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "note": f"{read_b + write_b} B/cell-step ({read_b} B forcing read + {write_b} B discharge/charge write) + "
@@ -626,18 +630,23 @@ def main():
                          "note": "2 * cells * (stations + 3) * chunk flops per call over its wall time "
                                  "(host part included)"},
         }
-    if pmc is not None and "launches" in pmc and "SQ_ACTIVE_INST_VALU" in pmc["launches"][0]:
-        # the bound that does apply: fp64 VALU issue. SQ_ACTIVE_INST_VALU (quad-cycles of VALU issue summed over
-        # waves, mean per launch over a year of chunks) over this run's kernel time on 1024 SIMDs at 2.4 GHz
-        act = float(np.mean([l["SQ_ACTIVE_INST_VALU"] for l in pmc["launches"]]))
-        ins = float(np.mean([l["SQ_INSTS_VALU"] for l in pmc["launches"]]))
+    if pmc is not None:
+        # the bound that does apply to the VALU-bound stacks: fp64 VALU issue. SQ_ACTIVE_INST_VALU (quad-cycles of
+        # VALU issue summed over waves) per timed launch of the same command, over this run's mean kernel time on
+        # 1024 SIMDs at 2.4 GHz
+        timed = pmc["launches"][pmc["warmup"]:]
+        act = float(np.mean([l["SQ_ACTIVE_INST_VALU"] for l in timed]))
+        ins = float(np.mean([l["SQ_INSTS_VALU"] for l in timed]))
         out["valu"] = {
             "busy": act * 4.0 / (1024 * 2.4e9 * avg_kernel_ms * 1e-3),
             "wave_instr_per_launch": ins,
             "lane_instr_per_cell_step": ins * 64.0 / (cells * chunk),
-            "by_chunk_busy": [round(l["valu_busy"], 3) for l in pmc["launches"]],
-            "source": "rocprofv3 SQ pass (profiles/r01/*_pmc.json); busy = SQ_ACTIVE_INST_VALU*4 / (1024 SIMDs x "
-                      "2.4 GHz x this run's mean kernel time); by_chunk_busy uses each PMC launch's own duration",
+            "by_chunk_busy": [round(l["valu_busy"], 3) for l in timed],
+            "profile_kernel_ms": pmc["trace_mean_ms_timed"],
+            "source": f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json (rocprofv3 SQ "
+                      "pass of this same command); busy = SQ_ACTIVE_INST_VALU*4 / (1024 SIMDs x 2.4 GHz x this "
+                      "run's mean kernel time); by_chunk_busy uses each PMC launch's own duration; "
+                      "profile_kernel_ms = the --kernel-trace pass's mean over the timed launches",
         }
     if router is not None:
         o = router.out[2]

@@ -1,23 +1,30 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench's dominant kernel, run from the repo root on the GPU box:
-#  1. --kernel-trace --stats of the default bench (same command as the bench line, minus cpu_baseline)
-#  2. separate --pmc passes (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass)
-#  3. one SQ pass (VALU instruction mix, wave cycles) for the fp64-VALU view of the kernel
-# Outputs under gpurun_out/prof_*; the summaries worth keeping are copied into profiles/ by hand.
+# rocprofv3 evidence for one bench line, run from the repo root on the GPU box. Every pass runs the SAME bench
+# command ($BENCH_ARGS, default = the driver's `--gpus 1 --steps 20 --warmup 5`):
+#  1. --kernel-trace --stats                (per-kernel durations; the line's kernel time must agree)
+#  2. --kernel-trace --pmc FETCH_SIZE        (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass)
+#  3. --kernel-trace --pmc WRITE_SIZE
+#  4. --kernel-trace --pmc SQ_*              (VALU issue: the bound that applies to the VALU-bound stacks)
+# then tools/pmc_summary.py writes profiles/$ROUND/pmc_<workload>.json, the file bench.py reads for the same
+# command's `traffic` / `valu` fields. Raw outputs stay under gpurun_out/prof_*; copy what is judged to profiles/.
 set -o pipefail
 R=$(pwd)
-ARGS=${BENCH_ARGS:-}
+ARGS=${BENCH_ARGS:---gpus 1 --steps 20 --warmup 5}
+ROUND=${ROUND:-r02}
+KERNEL=${KERNEL:-ptgsk_run_kernel}
 cd /tmp && export TMPDIR=/tmp
-run() {  # name, extra rocprofv3 args..., then bench args after --
+run() {  # name, rocprofv3 args...
     local name=$1; shift
-    timeout -k 10 600 rocprofv3 "$@" -d $R/gpurun_out/prof_$name -o run --output-format csv -- \
-        python3 $R/bench.py --no-cpu-baseline $ARGS $BARGS > $R/gpurun_out/prof_$name.log 2>&1 \
+    rm -rf $R/gpurun_out/prof_$name
+    timeout -k 10 400 rocprofv3 "$@" -d $R/gpurun_out/prof_$name -o run --output-format csv -- \
+        python3 $R/bench.py $ARGS > $R/gpurun_out/prof_$name.log 2>&1 \
         || { echo "PROF $name FAILED"; tail -20 $R/gpurun_out/prof_$name.log; exit 1; }
     echo "prof $name ok"
 }
-BARGS="--steps 12 --warmup 1" run trace --kernel-trace --stats
-BARGS="--steps 12 --warmup 0" run fetch --kernel-trace --pmc FETCH_SIZE
-BARGS="--steps 12 --warmup 0" run write --kernel-trace --pmc WRITE_SIZE
-BARGS="--steps 12 --warmup 0" run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
+run trace --kernel-trace --stats
+run fetch --kernel-trace --pmc FETCH_SIZE
+run write --kernel-trace --pmc WRITE_SIZE
+run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
 cd $R
+python3 tools/pmc_summary.py --kernel $KERNEL --round $ROUND --bench-args "$ARGS" || exit 1
 find gpurun_out -path "*prof_*" -name "*.csv" | sort

@@ -1,27 +1,38 @@
-"""Summarise the rocprofv3 passes of tools/gpu_profile.sh (gpurun_out/prof_{trace,fetch,write,sq}) for the
-bench's dominant kernel into profiles/<round>/<stack>_pmc.json, the file bench.py reads its `traffic` from.
+"""Summarise the rocprofv3 passes of tools/gpu_profile.sh (gpurun_out/prof_{trace,fetch,write,sq}) for one bench
+command into profiles/<round>/pmc_<workload>.json -- the file bench.py reads for that same command's `traffic`
+and `valu` fields.
 
-Per launch of the kernel (matched by dispatch order across the separate PMC passes, each a fresh run of the
-same bench command):
-  traffic  = FETCH_SIZE + WRITE_SIZE (KiB as reported -> bytes; no gfx950 x2 correction: the kernel's loads are
-             8 B/lane, a width MI355X_MICROARCH.md does not calibrate)
-  valu_busy = SQ_ACTIVE_INST_VALU * 4 / (SIMDs * duration * clock): the fraction of SIMD cycles issuing VALU
-             (SQ_ACTIVE_INST_* count quad-cycles; 1024 SIMDs; clock = 2.4 GHz, the MI355X maximum, so this is a
-             lower bound when the clock runs below it)
-  valu_instr_per_s = SQ_INSTS_VALU / duration (wave instructions)
-usage: python tools/pmc_summary.py <kernel-name-substring> <cells> <chunk> <out.json> [gpurun_out]
+Launches of the dominant kernel are matched by dispatch order across the passes (each pass is a fresh run of the
+same command); the first `warmup` launches are the bench's untimed warmup chunks and are reported apart. Over the
+timed launches:
+  fetch / write bytes: FETCH_SIZE and WRITE_SIZE (KiB -> bytes). MI355X_MICROARCH.md ("HBM [CDNA4]"): on gfx950
+      FETCH_SIZE reports half the bytes of a wide coalesced streaming read, WRITE_SIZE reads exactly. The kernels
+      here load and store 8 B per lane, a width the guide does not calibrate, so the same run calibrates it with
+      two kernels of known byte counts: the forcing generator writes exactly 40 B per cell-step (5 fp64 rows) and
+      the catchment segment sums read the 8 B discharge of every cell-step once. fetch_correction = algorithmic
+      read bytes / FETCH bytes of the segment sums (the guide's factor 2 when it holds), applied to the kernel's
+      FETCH; write_correction likewise from the generator.
+  traffic = fetch * fetch_correction + write * write_correction per launch
+  valu_busy = SQ_ACTIVE_INST_VALU * 4 / (1024 SIMDs * duration * 2.4 GHz) (quad-cycles of VALU issue; a lower
+      bound if the clock runs below its 2.4 GHz maximum)
+  trace_mean_ms: the kernel's mean duration in the --kernel-trace --stats pass (timed launches; all launches too)
+usage: python tools/pmc_summary.py [--kernel K] [--round r02] [--bench-args "..."] [--base gpurun_out]
 """
+import argparse
 import csv
 import json
 import os
+import shlex
 import sys
 from collections import defaultdict
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 SIMDS = 256 * 4
 CLOCK = 2.4e9
 
 
-def launches(path, kname):
+def counter_rows(path, kname):
     rows = defaultdict(dict)
     meta = {}
     for r in csv.DictReader(open(path)):
@@ -34,38 +45,95 @@ def launches(path, kname):
     return [(d, rows[d], meta[d]) for d in sorted(rows)]
 
 
+def trace_durations(path, kname):
+    out = []
+    for r in csv.DictReader(open(path)):
+        if kname in r["Kernel_Name"]:
+            out.append((int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+    return [ms for _, ms in sorted(out)]
+
+
+def mean(v):
+    return sum(v) / len(v) if v else float("nan")
+
+
 def main():
-    kname, cells, chunk, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    base = sys.argv[5] if len(sys.argv) > 5 else "gpurun_out"
-    f = launches(os.path.join(base, "prof_fetch", "run_counter_collection.csv"), kname)
-    w = launches(os.path.join(base, "prof_write", "run_counter_collection.csv"), kname)
-    q = launches(os.path.join(base, "prof_sq", "run_counter_collection.csv"), kname)
-    res = {"command": "tools/gpu_profile.sh: rocprofv3 --kernel-trace --pmc <counters> -- python3 bench.py "
-                      "--no-cpu-baseline --steps 12 --warmup 0 (one pass per counter group; a full year of 730-step chunks)",
-           "kernel": kname, "cells": cells, "chunk": chunk, "launches": []}
-    fetch, write, busy, ips = [], [], [], []
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="ptgsk_run_kernel")
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--bench-args", default="--gpus 1 --steps 20 --warmup 5")
+    ap.add_argument("--base", default=os.path.join(ROOT, "gpurun_out"))
+    o = ap.parse_args()
+    import bench
+    a = bench.parse(shlex.split(o.bench_args))
+    L = bench.Layout(a, 1, 0)
+    cells, chunk, W = L.n, a.chunk, a.warmup
+    read_b, write_b, state_b, _ = bench.STACKS[a.stack]
+
+    f = counter_rows(os.path.join(o.base, "prof_fetch", "run_counter_collection.csv"), o.kernel)
+    w = counter_rows(os.path.join(o.base, "prof_write", "run_counter_collection.csv"), o.kernel)
+    q = counter_rows(os.path.join(o.base, "prof_sq", "run_counter_collection.csv"), o.kernel)
+    if not f or len(f) != len(w) or len(f) != len(q):
+        raise SystemExit(f"launch counts differ across passes: {len(f)} {len(w)} {len(q)}")
+    # calibration kernels (same runs)
+    gen_w = counter_rows(os.path.join(o.base, "prof_write", "run_counter_collection.csv"), "synthetic_forcing_kernel")
+    seg_f = counter_rows(os.path.join(o.base, "prof_fetch", "run_counter_collection.csv"), "segment_sum_kernel")
+    gen_bytes = cells * chunk * 40.0
+    seg_bytes = cells * chunk * 8.0
+    gmax = max([m["grid"] for _, _, m in gen_w], default=0)   # the region's launches (not cpu_baseline's sample)
+    write_ratio = mean([r["WRITE_SIZE"] * 1024.0 / gen_bytes for _, r, m in gen_w if m["grid"] == gmax]) if gen_w else None
+    seg_ratios = [r["FETCH_SIZE"] * 1024.0 / seg_bytes for _, r, m in seg_f if m["grid"] >= chunk * 256]
+    fetch_ratio = mean(seg_ratios) if seg_ratios else None
+    fetch_corr = 1.0 / fetch_ratio if fetch_ratio else 2.0
+    write_corr = 1.0 / write_ratio if write_ratio else 1.0
+
+    launches = []
     for (df, cf, mf), (dw, cw, mw), (dq, cq, mq) in zip(f, w, q):
         fb = cf["FETCH_SIZE"] * 1024.0
         wb = cw["WRITE_SIZE"] * 1024.0
         dur = mq["duration_ns"] * 1e-9
-        vb = cq["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * dur * CLOCK)
-        fetch.append(fb)
-        write.append(wb)
-        busy.append(vb)
-        ips.append(cq["SQ_INSTS_VALU"] / dur)
-        res["launches"].append({"dispatch": [df, dw, dq], "fetch_bytes": fb, "write_bytes": wb,
-                                "sq_duration_ns": mq["duration_ns"], "valu_busy": vb, **cq, **mq})
-    n = len(fetch)
-    if n == 0:
-        raise SystemExit("no launches of " + kname)
-    res["fetch_bytes_per_launch"] = sum(fetch) / n
-    res["write_bytes_per_launch"] = sum(write) / n
-    res["traffic_bytes_per_launch"] = (sum(fetch) + sum(write)) / n
-    res["valu_busy"] = sum(busy) / n
-    res["valu_wave_instr_per_s"] = sum(ips) / n
-    res["algorithmic_bytes_per_launch"] = cells * chunk * 56 + cells * 144
+        launches.append({"dispatch": [df, dw, dq], "fetch_bytes": fb, "write_bytes": wb,
+                         "traffic_bytes": fb * fetch_corr + wb * write_corr,
+                         "sq_duration_ns": mq["duration_ns"],
+                         "valu_busy": cq["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * dur * CLOCK), **cq, **mq})
+    timed = launches[W:]
+    tr = trace_durations(os.path.join(o.base, "prof_trace", "run_kernel_trace.csv"), o.kernel)
+    algo = cells * chunk * (read_b + write_b) + cells * state_b
+    res = {
+        "command": f"python3 bench.py {o.bench_args} under rocprofv3 (tools/gpu_profile.sh: one --kernel-trace "
+                   f"--stats pass, then one --pmc pass per counter group, each a fresh run of the same command)",
+        "workload": bench.workload_tag(a, cells),
+        "kernel": o.kernel, "cells": cells, "chunk": chunk, "steps": a.steps, "warmup": W,
+        "calibration": {
+            "write_ratio_generator": write_ratio,
+            "fetch_ratio_segment_sum": fetch_ratio,
+            "fetch_correction": fetch_corr, "write_correction": write_corr,
+            "note": "ratio = counter bytes / known bytes of the same run's forcing generator (40 B/cell-step "
+                    "written) and catchment segment sums (8 B/cell-step read); corrections are 1/ratio",
+        },
+        "algorithmic_bytes_per_launch": algo,
+        "fetch_bytes_per_launch": mean([l["fetch_bytes"] for l in timed]),
+        "write_bytes_per_launch": mean([l["write_bytes"] for l in timed]),
+        "traffic_bytes_per_launch": mean([l["traffic_bytes"] for l in timed]),
+        "valu_busy": mean([l["valu_busy"] for l in timed]),
+        "valu_wave_instr_per_launch": mean([l["SQ_INSTS_VALU"] for l in timed]),
+        "trace_mean_ms_timed": mean(tr[W:]),
+        "trace_mean_ms_all": mean(tr),
+        "trace_launches": len(tr),
+        "launches": launches,
+    }
+    res["traffic_over_algorithmic"] = res["traffic_bytes_per_launch"] / algo
+    out_dir = os.path.join(ROOT, "profiles", o.round)
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"pmc_{res['workload']}.json")
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps({k: res[k] for k in ("traffic_bytes_per_launch", "valu_busy", "valu_wave_instr_per_s")}))
+    import shutil
+    stats = os.path.join(o.base, "prof_trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(out_dir, f"stats_{res['workload']}.csv"))
+    print(out)
+    print(json.dumps({k: res[k] for k in ("traffic_bytes_per_launch", "traffic_over_algorithmic", "valu_busy",
+                                          "trace_mean_ms_timed", "trace_mean_ms_all", "calibration")}))
 
 
 if __name__ == "__main__":
