@@ -198,6 +198,7 @@ DM_FN double pow(double x, double y) {
     if (y == 0.0) return 1.0;
     if (x == 1.0) return 1.0;
     if (y == 1.0) return x;  // exact, as a correctly rounded pow (distance_measure with factor 2)
+    if (y == 2.0) return x * x;  // the correctly rounded square (hbv_soil's default beta = 2, hbv_soil.h:19-24)
     if (is_nan(x) || is_nan(y)) return qnan();
     const double ax = x < 0 ? -x : x;
     const double ay = y < 0 ? -y : y;

@@ -272,6 +272,15 @@ extern "C" void oracle_gamma_pq(double a, double x, double* p, double* p1, doubl
     *prefix = r.prefix;
 }
 
+// gamma_pq at gamma_snow's boost precision policy (digits10<10> for a < 2, digits10<5> otherwise,
+// gamma_snow.h:189-197): the evaluation calc_snow_state and calc_q make
+extern "C" void oracle_gamma_pq_policy(double a, double x, double* p, double* p1, double* prefix) {
+    const auto r = special::gamma_pq(a, x, detmath::gamma_snow_policy_eps(a));
+    *p = r.p;
+    *p1 = r.p1;
+    *prefix = r.prefix;
+}
+
 // ---------------------------------------------------------------- hbv_stack
 // Snow distribution row per parameter set: n_bins, s[8], intervals[8] (17 doubles).
 namespace {

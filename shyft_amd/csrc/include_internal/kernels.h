@@ -48,6 +48,7 @@ struct hbv_kargs {
     double* state_series;    // [HBV_NS][win_len+1][N] or null
     const uint8_t* active;   // [N] or null
     int32_t* err;            // [N]
+    int uniform_params;      // 1: every cell uses parameter set 0 (n_sets == 1)
 };
 
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream);

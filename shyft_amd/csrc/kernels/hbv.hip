@@ -20,8 +20,11 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-#ifndef SHYFT_HBV_PREFETCH
-#define SHYFT_HBV_PREFETCH 1
+// forcing prefetch depth: steps i+1 .. i+D are in flight while step i computes. The kernel moves 48 B per
+// cell-step and does little arithmetic per byte, so its HBM rate is set by the bytes in flight (Little's law):
+// at 2 waves per SIMD one step ahead keeps ~16 KB per CU in flight.
+#ifndef SHYFT_HBV_PF
+#define SHYFT_HBV_PF 1
 #endif
 
 // occupancy target (waves per SIMD; variant builds override with -DSHYFT_HBV_WAVES=N, 0 = the compiler's choice)
@@ -34,6 +37,9 @@ constexpr int BLOCK = 256;
 #define SHYFT_HBV_OCC
 #endif
 
+// UNIFORM: every cell uses parameter set 0, so the parameter row (incl. the bin distribution s[], I[]) is
+// wave-uniform and lives in SGPRs instead of 2 x 8 + 15 per-lane doubles of VGPRs
+template <bool UNIFORM>
 __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
@@ -42,7 +48,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     // forcing column: the lane itself, or the shared cell of a parameter-ensemble lane
     const size_t NF = a.fcol ? (size_t)a.f_cols : N;
     const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * HBV_NP;
+    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * HBV_NP;
 
     hbv_snow_par sp_par;
     sp_par.nb = (int)P[HK_NB];
@@ -114,26 +120,29 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     };
 
     const int i_end = a.step0 + a.n_steps;
-    // the next step's forcing is loaded before this step's arithmetic, so its HBM latency overlaps the step
-    // instead of stalling the top of every iteration (the kernel is latency-bound at 3 waves per SIMD)
-    double nx_temp = 0, nx_rad = 0, nx_rh = 0, nx_prec = 0;
-    if (SHYFT_HBV_PREFETCH && a.step0 < i_end) {
-        const size_t ff = (size_t)(a.step0 - a.win0) * NF + fcl;
-        nx_temp = f_temp[ff]; nx_rad = f_rad[ff]; nx_rh = f_rh[ff]; nx_prec = f_prec[ff];
+    // the next D steps' forcing is loaded before this step's arithmetic, so its HBM latency overlaps D steps
+    // instead of stalling the top of every iteration
+    constexpr int D = SHYFT_HBV_PF;
+    double rt[D], rr[D], rh[D], rp[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        rt[k] = rr[k] = rh[k] = rp[k] = 0.0;
+        if (a.step0 + k < i_end) {
+            const size_t ff = (size_t)(a.step0 + k - a.win0) * NF + fcl;
+            rt[k] = f_temp[ff]; rr[k] = f_rad[ff]; rh[k] = f_rh[ff]; rp[k] = f_prec[ff];
+        }
     }
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
-        double temp, rad, rel_hum, prec_raw;
-        if (SHYFT_HBV_PREFETCH) {
-            temp = nx_temp; rad = nx_rad; rel_hum = nx_rh; prec_raw = nx_prec;
-            if (i + 1 < i_end) {
-                const size_t fn = (wi + 1) * NF + fcl;
-                nx_temp = f_temp[fn]; nx_rad = f_rad[fn]; nx_rh = f_rh[fn]; nx_prec = f_prec[fn];
-            }
-        } else {
-            const size_t ff = wi * NF + fcl;
-            temp = f_temp[ff]; rad = f_rad[ff]; rel_hum = f_rh[ff]; prec_raw = f_prec[ff];
+        const double temp = rt[0], rad = rr[0], rel_hum = rh[0], prec_raw = rp[0];
+#pragma unroll
+        for (int k = 0; k + 1 < D; ++k) {
+            rt[k] = rt[k + 1]; rr[k] = rr[k + 1]; rh[k] = rh[k + 1]; rp[k] = rp[k + 1];
+        }
+        if (i + D < i_end) {
+            const size_t fn = (wi + D) * NF + fcl;
+            rt[D - 1] = f_temp[fn]; rr[D - 1] = f_rad[fn]; rh[D - 1] = f_rh[fn]; rp[D - 1] = f_prec[fn];
         }
         const double prec = prec_raw * p_corr;
         if (SS) collect_state(wi);
@@ -205,6 +214,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(hbv_run_kernel, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (a.uniform_params) hipLaunchKernelGGL(hbv_run_kernel<true>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    else hipLaunchKernelGGL(hbv_run_kernel<false>, dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

@@ -1048,6 +1048,7 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
         a.active = h->active.empty() ? nullptr : h->d_active.p;
         a.err = h->d_err.p;
+        a.uniform_params = h->n_sets == 1 ? 1 : 0;
         hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
         hip_check(launch_hbv_run(a, h->stream), "hbv_run_kernel launch");
         hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");

@@ -42,6 +42,7 @@ def load(variant: str = "detmath"):
     L.oracle_gamma_p.restype = _d
     L.oracle_gamma_p.argtypes = [_d, _d]
     L.oracle_gamma_pq.argtypes = [_d, _d, _dp, _dp, _dp]
+    L.oracle_gamma_pq_policy.argtypes = [_d, _d, _dp, _dp, _dp]
     L.oracle_lgamma.restype = _d
     L.oracle_lgamma.argtypes = [_d]
     L.oracle_gs_calc_snow_state.argtypes = [_d] * 7 + [_dp, _dp]
