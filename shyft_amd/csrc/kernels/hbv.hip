@@ -29,13 +29,16 @@ constexpr int BLOCK = 256;
 
 // occupancy target (waves per SIMD; variant builds override with -DSHYFT_HBV_WAVES=N, 0 = the compiler's choice)
 #ifndef SHYFT_HBV_WAVES
-#define SHYFT_HBV_WAVES 2  // measured without the forcing prefetch: compiler choice (2) 19.2 ms, 3: 18.5, 4: 20.8; with it: 2: 14.9, 3: 16.3, 4: 23.1
+// measured (512K cells, ms per 730-step chunk, year mean): per-lane parameter rows: 2 waves 15.0, 3: 16.3,
+// 4: 23.1; uniform rows in SGPRs (the default launch): 2: 13.8, 3: 11.5, 4: 11.0, 5: 17.6. Prefetch depth 1-4
+// and LDS-resident bin arrays measured no better.
+#define SHYFT_HBV_WAVES 4
 #endif
-#if SHYFT_HBV_WAVES > 0
-#define SHYFT_HBV_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_HBV_WAVES, SHYFT_HBV_WAVES)))
-#else
-#define SHYFT_HBV_OCC
+#ifndef SHYFT_HBV_WAVES_PERLANE
+#define SHYFT_HBV_WAVES_PERLANE 2  // the per-lane-parameter launch (catchment parameter sets)
 #endif
+#define SHYFT_HBV_OCC __attribute__((amdgpu_waves_per_eu(UNIFORM ? SHYFT_HBV_WAVES : SHYFT_HBV_WAVES_PERLANE, \
+                                                         UNIFORM ? SHYFT_HBV_WAVES : SHYFT_HBV_WAVES_PERLANE)))
 
 // UNIFORM: every cell uses parameter set 0, so the parameter row (incl. the bin distribution s[], I[]) is
 // wave-uniform and lives in SGPRs instead of 2 x 8 + 15 per-lane doubles of VGPRs
