@@ -80,9 +80,13 @@ def main():
     seg_f = counter_rows(os.path.join(o.base, "prof_fetch", "run_counter_collection.csv"), "segment_sum_kernel")
     gen_bytes = cells * chunk * 40.0
     seg_bytes = cells * chunk * 8.0
-    gmax = max([m["grid"] for _, _, m in gen_w], default=0)   # the region's launches (not cpu_baseline's sample)
-    write_ratio = mean([r["WRITE_SIZE"] * 1024.0 / gen_bytes for _, r, m in gen_w if m["grid"] == gmax]) if gen_w else None
-    seg_ratios = [r["FETCH_SIZE"] * 1024.0 / seg_bytes for _, r, m in seg_f if m["grid"] >= chunk * 256]
+    # the region's generator launches (not cpu_baseline's 4000-cell sample; --idw runs have none)
+    gen_w = [g for g in gen_w if g[2]["grid"] >= cells]
+    write_ratio = mean([r["WRITE_SIZE"] * 1024.0 / gen_bytes for _, r, m in gen_w]) if gen_w else None
+    # the catchment sums (one workgroup per step and catchment, contiguous cell blocks, so coalesced rows);
+    # routing group sums use the same kernel on hash-scattered cells (gathers) and are not a calibration
+    seg_grid = chunk * L.n_catch * 256
+    seg_ratios = [r["FETCH_SIZE"] * 1024.0 / seg_bytes for _, r, m in seg_f if m["grid"] == seg_grid]
     fetch_ratio = mean(seg_ratios) if seg_ratios else None
     fetch_corr = 1.0 / fetch_ratio if fetch_ratio else 2.0
     write_corr = 1.0 / write_ratio if write_ratio else 1.0
