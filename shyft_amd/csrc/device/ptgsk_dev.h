@@ -77,13 +77,21 @@ __device__ inline double gs_calc_q(double a, double b, double z, double lga) {
 
 // corr_lwc (gamma_snow.h:214-227): boost brent_find_minima over [0, z1],
 // 12 bits, 60 iterations; golden constant is the float literal 0.3819660f.
-__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2) {
+#ifdef SHYFT_PROF
+#define SHYFT_PROF_NF , int& nf_evals
+#else
+#define SHYFT_PROF_NF
+#endif
+__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2 SHYFT_PROF_NF) {
 #ifdef SHYFT_ABLATE_BRENT
     return z1 * 0.5;  // timing ablation only (wrong results)
 #endif
     const double Q1 = gs_calc_q(a1, b1, z1, dlgamma(a1));
     const double lga2 = dlgamma(a2);
     auto f = [&](double z) {
+#ifdef SHYFT_PROF
+        ++nf_evals;
+#endif
         const double v = gs_calc_q(a2, b2, z, lga2) - Q1;
         return v * v;
     };
@@ -163,9 +171,20 @@ struct gs_mid {
         iso_pot_energy, potential_melt, start_storage, sdc_scale;
 };
 
+// The snow storage of the state as it leaves a step: gs_back's final calc_snow_state(alpha, sdc_melt_mean/alpha,
+// ibgf, acc_melt, lwc, ...) -- exactly the call gs_front opens the next step with (same state fields, and
+// gs_back always leaves sdc_scale == sdc_melt_mean / alpha), unless the winter-end day resets acc_melt in between
+// or the step took the early no-snow path. gs_front then reuses the value instead of evaluating the incomplete
+// gamma functions again: same function of the same arguments, so the same bits (gamma_snow.h:359 vs :459).
+struct gs_carry {
+    double storage = 0.0;
+    bool ok = false;
+};
+
 __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
                                       const double* __restrict__ P, const gs_cell& cc, double T, double rad,
-                                      double prec_mm_h, double wind_speed, double rel_hum, lgamma_cache& lgc) {
+                                      double prec_mm_h, double wind_speed, double rel_hum, lgamma_cache& lgc,
+                                      const gs_carry& carry) {
     m.need = false;
     m.done = false;
     double sdc_melt_mean = s.sdc_melt_mean;
@@ -231,7 +250,8 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
     const double potential_melt = smax(0.0, energy / 333660.0);
 
     double sdc_scale = sdc_melt_mean / alpha;
-    calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
+    if (carry.ok && !start_melt) storage = carry.storage;  // sca of this call is not used by gs_back
+    else calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
     m.start_storage = storage;
 
     if (acc_melt < 0.0) {
@@ -271,8 +291,9 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
 
 __device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, double& r_sca, double& r_storage,
                                      double& r_outflow, bool snow_season, double dt_us, const double* __restrict__ P,
-                                     const gs_cell& cc, double prec_mm_h, lgamma_cache& lgc) {
+                                     const gs_cell& cc, double prec_mm_h, lgamma_cache& lgc, gs_carry& carry) {
     if (m.done) {
+        carry.ok = false;
         s.albedo = P[PK_MAX_ALBEDO];
         s.surface_heat = 0.0;
         s.iso_pot_energy = 0.0;
@@ -339,6 +360,8 @@ __device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, dou
         }
     }
     calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
+    carry.storage = storage;
+    carry.ok = true;
     double outflow = m.prec + m.start_storage - storage;
     if (outflow < 0.0) outflow = 0.0;
 
@@ -355,7 +378,14 @@ __device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, dou
     r_outflow = (outflow * 3600000000.0) / dt_us;
 }
 
-__device__ inline double gs_solve_lwc(const gs_mid& m) { return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2); }
+__device__ inline double gs_solve_lwc(const gs_mid& m) {
+#ifdef SHYFT_PROF
+    int nf = 0;
+    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2, nf);
+#else
+    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2);
+#endif
+}
 
 // ------------------------------------------------------------------ kirchner
 // kirchner.h:186-198

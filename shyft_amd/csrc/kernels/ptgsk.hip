@@ -24,10 +24,10 @@ using namespace shyft_dev;
 
 #ifdef SHYFT_PROF
 // phase timing (profiling builds only): per-wavefront s_memtime deltas summed over the launch
-__device__ unsigned long long g_ptgsk_prof[8];
+__device__ unsigned long long g_ptgsk_prof[12];
 extern "C" int shyft_ptgsk_prof_read(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptgsk_prof), sizeof(g_ptgsk_prof)) != hipSuccess) return 1;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[12] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_ptgsk_prof), z, sizeof z) != hipSuccess;
 }
 #define PROF_DECL unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long prof_t = __builtin_amdgcn_s_memtime();
@@ -48,6 +48,11 @@ constexpr int BLOCK = SHYFT_BLOCK;
 
 #ifndef SHYFT_LB_WAVES
 #define SHYFT_LB_WAVES 4
+#endif
+
+// issue priority (s_setprio) of the Brent-solving wavefront: 138.2 -> 134.5 ms per chunk (year mean, 1M cells)
+#ifndef SHYFT_BRENT_PRIO
+#define SHYFT_BRENT_PRIO 3
 #endif
 
 // UNIFORM: every cell of the launch uses parameter set 0 (the region parameter, no catchment overrides):
@@ -96,6 +101,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     s.temp_swe = st[PS_TEMP_SWE * N + lc];
     double q = st[PS_KIRCHNER_Q * N + lc];
     lgamma_cache lgc;
+    gs_carry carry;
     int32_t err = 0;
 
     const size_t TW = (size_t)a.win_len;
@@ -161,7 +167,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
         m.need = false;
         m.done = true;
         if (valid)
-            gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc);
+            gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc, carry);
         PROF_MARK(0);  // forcing + gs_front
         double z = 0.0;
         if (COMPACT) {
@@ -175,7 +181,40 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
             PROF_MARK(1);  // job queue + barrier
             const int nj = jcount[i & 1];
             if (nj > 0) {
-                for (int j = threadIdx.x; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j]);
+#ifdef SHYFT_PROF
+                const unsigned long long tb = __builtin_amdgcn_s_memtime();
+                int nf = 0;
+                for (int j = threadIdx.x; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], nf);
+                if (threadIdx.x < nj) {  // solver lanes: wave sum and wave max of f evaluations
+                    int sum = nf, mx = nf;
+                    for (int o = 32; o > 0; o >>= 1) {
+                        sum += __shfl_xor(sum, o, 64);
+                        const int m2 = __shfl_xor(mx, o, 64);
+                        mx = m2 > mx ? m2 : mx;
+                    }
+                    if ((threadIdx.x & 63) == 0) {
+                        atomicAdd(&g_ptgsk_prof[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb));
+                        atomicAdd(&g_ptgsk_prof[9], (unsigned long long)mx);
+                        atomicAdd(&g_ptgsk_prof[10], (unsigned long long)sum);
+                    }
+                }
+#else
+#ifdef SHYFT_ROTATE2
+                // the solving wavefront rotates with the step and the workgroup (SIMD load balance)
+                const int t = (threadIdx.x + BLOCK - 64 * ((i + (int)blockIdx.x) % (BLOCK / 64))) % BLOCK;
+#else
+                const int t = threadIdx.x;
+#endif
+#if SHYFT_BRENT_PRIO > 0
+                // the solving wavefront is the workgroup's critical path (its other wavefronts wait at the
+                // barrier below): it gets issue priority over the other workgroups' wavefronts on its SIMD
+                if (t < nj) __builtin_amdgcn_s_setprio(SHYFT_BRENT_PRIO);
+#endif
+                for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j]);
+#if SHYFT_BRENT_PRIO > 0
+                __builtin_amdgcn_s_setprio(0);
+#endif
+#endif
                 __syncthreads();
                 if (slot >= 0) z = jres[slot];
             }
@@ -185,7 +224,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
         PROF_MARK(2);  // Brent phase
         if (!valid) continue;
         double gs_sca, gs_storage, gs_outflow;
-        gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc);
+        gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc, carry);
         PROF_MARK(3);  // gs_back
 
         // glacier_melt::step (glacier_melt.h:47-52)
@@ -196,6 +235,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
         const double pot_evap = pt_pot_evap(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum) * 3600.0;
         const double ae = pot_evap * (1.0 - dexp(-q * 3.0 / P[PK_AE_SCALE])) * (1.0 - smax(gs_sca, glacier_fraction));
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
+        PROF_MARK(4);  // glacier, PT, AE
         double q_avg;
         if (!kirchner_step(q, q_avg, gs_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
                            ae, a.t1_hours, kc1, kc2, kc3))
@@ -219,7 +259,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
             R[7 * RS + fo] = pot_evap;
         }
         if (SS && i + 1 == i_end) collect_state(wi + 1);
-        PROF_MARK(4);  // glacier, PT, AE, kirchner, outputs
+        PROF_MARK(5);  // kirchner, outputs
     }
     PROF_FLUSH();
     if (!valid) return;

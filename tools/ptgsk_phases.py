@@ -3,7 +3,7 @@
 usage (GPU box): python tools/ptgsk_phases.py lib.so [cells]
 Runs the bench region from Jan 1 through 12 chunks of 730 steps and prints, per chunk, the kernel ms and the
 share of wavefront time in: front (forcing + gs_front), queue (job queue + barrier), brent (Brent phase incl.
-its barriers), back (gs_back), rest (glacier, PT, AE, kirchner, outputs)."""
+its barriers), back (gs_back), pt+ae (glacier, PT, AE), kirchner (kirchner, outputs)."""
 import ctypes as C
 import os
 import sys
@@ -18,7 +18,7 @@ from shyft_amd import _native  # noqa: E402
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 L = _native.lib()
 L.shyft_ptgsk_prof_read.argtypes = [C.c_void_p]
-buf = (C.c_ulonglong * 8)()
+buf = (C.c_ulonglong * 12)()
 r = HipRegion(PT_GS_K, N, device=0)
 r.set_geo(synthetic.geo11(N, n_catchments=100))
 r.set_parameters(synthetic.default_ptgsk_parameters())
@@ -26,12 +26,16 @@ r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, 8760, 730)
 r.set_collection(COLLECT_DISCHARGE)
 r.set_state(synthetic.default_ptgsk_state(N))
 L.shyft_ptgsk_prof_read(buf)
-names = ("front", "queue", "brent", "back", "rest")
+names = ("front", "queue", "brent", "back", "pt+ae", "kirchner")
 for s in range(12):
     r.move_window(s * 730, 0)
     r.synthetic_forcing(synthetic.SEED, s * 730, 730)
     r.run_cells(0, s * 730, 730)
     L.shyft_ptgsk_prof_read(buf)
-    tot = sum(buf[k] for k in range(5)) or 1
+    tot = sum(buf[k] for k in range(6)) or 1
+    extra = ""
+    if buf[9]:
+        # solver waves: cycles per Brent loop trip (wave max of f evaluations), and useful lanes per trip
+        extra = f"  solver: {buf[8] / buf[9]:7.0f} cyc/trip, {buf[10] / buf[9]:4.1f} lane-evals/trip"
     print(f"chunk {s:2d} {r.last_run_ms():6.1f} ms  " +
-          "  ".join(f"{n} {100.0 * buf[k] / tot:4.1f}%" for k, n in enumerate(names)), flush=True)
+          "  ".join(f"{n} {100.0 * buf[k] / tot:4.1f}%" for k, n in enumerate(names)) + extra, flush=True)
