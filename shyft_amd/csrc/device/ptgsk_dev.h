@@ -34,10 +34,18 @@ struct lgamma_cache {
     }
 };
 
+// P(shape, x) and P(shape+1, x) of calc_snow_state's liquid-water evaluation, x = (lwd / max_water) / scale,
+// or NaN when the call did not make it. corr_lwc's Q1 = calc_q(alpha_prev, scale_prev, lwc / max_water)
+// (gamma_snow.h:225) is the same gamma_p pair at the same point when the step's first calc_snow_state made it.
+struct gs_lw {
+    double p = __builtin_nan(""), p1 = __builtin_nan("");
+};
+
 // gamma_snow.h:230-260
 __device__ SHYFT_INL_SNOW void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
                                        double max_water_frac, double temp_swe, double& swe, double& sca,
-                                       lgamma_cache& lgc) {
+                                       lgamma_cache& lgc, gs_lw& lw) {
+    lw.p = lw.p1 = __builtin_nan("");
     double y = 0.0, y1 = 0.0;
     const double m = shape * scale;
     if (lambda <= 0.0) {
@@ -60,6 +68,8 @@ __device__ SHYFT_INL_SNOW void calc_snow_state(double shape, double scale, doubl
         const double sat = lwd / max_water_frac;
         const double x = sat / scale;
         const gamma_p_result g = gs_gamma_pq(shape, x, lgc.get(shape));
+        lw.p = g.p;
+        lw.p1 = g.p1;
         const double ssa = g.p;
         const double ssa1 = ssa - g.prefix / shape;
         const double liqwat = max_water_frac * (m * (ssa1 - y1) + sat * (1.0 - ssa) - lambda * (1.0 - y));
@@ -82,12 +92,16 @@ __device__ inline double gs_calc_q(double a, double b, double z, double lga) {
 #else
 #define SHYFT_PROF_NF
 #endif
-__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2 SHYFT_PROF_NF) {
+// q1: Q1 = calc_q(a1, b1, z1) when the caller already has it (from the step's first calc_snow_state, gs_lw),
+// else NaN
+// lga2 = lgamma(a2): the job's lane evaluates it (its lgamma cache needs it for the step's calc_snow_state after
+// the solve anyway), so the solving wavefront does not
+__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2,
+                                           double q1, double lga2 SHYFT_PROF_NF) {
 #ifdef SHYFT_ABLATE_BRENT
     return z1 * 0.5;  // timing ablation only (wrong results)
 #endif
-    const double Q1 = gs_calc_q(a1, b1, z1, dlgamma(a1));
-    const double lga2 = dlgamma(a2);
+    const double Q1 = q1 == q1 ? q1 : gs_calc_q(a1, b1, z1, dlgamma(a1));
     auto f = [&](double z) {
 #ifdef SHYFT_PROF
         ++nf_evals;
@@ -165,8 +179,8 @@ struct gs_cell {
 // evaluates them).
 struct gs_mid {
     bool done;  // the early "no snow" path was taken (gamma_snow.h:313-322)
-    bool need;  // corr_lwc job: z1, a1, b1, a2, b2
-    double z1, a1, b1, a2, b2;
+    bool need;  // corr_lwc job: z1, a1, b1, a2, b2 (+ q1 = calc_q(a1, b1, z1) or NaN, lga2 = lgamma(a2))
+    double z1, a1, b1, a2, b2, q1, lga2;
     double prec, snow, rain, albedo, lwc, surface_heat, alpha, temp_swe, sca, storage, sdc_melt_mean, acc_melt,
         iso_pot_energy, potential_melt, start_storage, sdc_scale;
 };
@@ -178,6 +192,7 @@ struct gs_mid {
 // gamma functions again: same function of the same arguments, so the same bits (gamma_snow.h:359 vs :459).
 struct gs_carry {
     double storage = 0.0;
+    gs_lw lw;
     bool ok = false;
 };
 
@@ -250,8 +265,13 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
     const double potential_melt = smax(0.0, energy / 333660.0);
 
     double sdc_scale = sdc_melt_mean / alpha;
-    if (carry.ok && !start_melt) storage = carry.storage;  // sca of this call is not used by gs_back
-    else calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
+    gs_lw lw;
+    if (carry.ok && !start_melt) {
+        storage = carry.storage;  // sca of this call is not used by gs_back
+        lw = carry.lw;
+    } else {
+        calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc, lw);
+    }
     m.start_storage = storage;
 
     if (acc_melt < 0.0) {
@@ -271,6 +291,11 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
                 m.b1 = sdc_scale_prev > 0.0 ? sdc_scale_prev : sdc_scale;
                 m.a2 = alpha;
                 m.b2 = sdc_scale;
+                // calc_q(a1, b1, z1) = a1 b1 P(a1+1, z1/b1) + z1 (1 - P(a1, z1/b1)) (gamma_snow.h:209-212) from the
+                // opening calc_snow_state's liquid-water pair (same shape, scale and point, z1 / b1 = sat / scale)
+                m.q1 = (sdc_scale_prev > 0.0 && lw.p == lw.p) ? m.a1 * m.b1 * lw.p1 + m.z1 * (1.0 - lw.p)
+                                                               : __builtin_nan("");
+                m.lga2 = lgc.get(alpha);
             }
         }
     }
@@ -313,7 +338,8 @@ __device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, dou
     if (acc_melt < 0.0) {
         if (m.need) {
             lwc = z * max_water;
-            calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
+            gs_lw lw2;
+            calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc, lw2);
         }
         lwc += rain;
         if (sdc_melt_mean <= potential_melt) {
@@ -359,7 +385,7 @@ __device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, dou
             }
         }
     }
-    calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc);
+    calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc, carry.lw);
     carry.storage = storage;
     carry.ok = true;
     double outflow = m.prec + m.start_storage - storage;
@@ -381,9 +407,9 @@ __device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, dou
 __device__ inline double gs_solve_lwc(const gs_mid& m) {
 #ifdef SHYFT_PROF
     int nf = 0;
-    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2, nf);
+    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2, m.q1, m.lga2, nf);
 #else
-    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2);
+    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2, m.q1, m.lga2);
 #endif
 }
 

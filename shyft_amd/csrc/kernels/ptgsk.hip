@@ -119,7 +119,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
 
     // Brent job queue of the workgroup (COMPACT)
-    __shared__ double jz1[BLOCK], ja1[BLOCK], jb1[BLOCK], ja2[BLOCK], jb2[BLOCK], jres[BLOCK];
+    __shared__ double jz1[BLOCK], ja1[BLOCK], jb1[BLOCK], ja2[BLOCK], jb2[BLOCK], jq1[BLOCK], jlg2[BLOCK], jres[BLOCK];
     __shared__ int jcount[2];
     if (COMPACT) {
         if (threadIdx.x == 0) jcount[0] = 0;
@@ -176,6 +176,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
             if (m.need) {
                 slot = atomicAdd(&jcount[i & 1], 1);
                 jz1[slot] = m.z1; ja1[slot] = m.a1; jb1[slot] = m.b1; ja2[slot] = m.a2; jb2[slot] = m.b2;
+                jq1[slot] = m.q1; jlg2[slot] = m.lga2;
             }
             __syncthreads();
             PROF_MARK(1);  // job queue + barrier
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
 #ifdef SHYFT_PROF
                 const unsigned long long tb = __builtin_amdgcn_s_memtime();
                 int nf = 0;
-                for (int j = threadIdx.x; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], nf);
+                for (int j = threadIdx.x; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j], nf);
                 if (threadIdx.x < nj) {  // solver lanes: wave sum and wave max of f evaluations
                     int sum = nf, mx = nf;
                     for (int o = 32; o > 0; o >>= 1) {
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
                 // barrier below): it gets issue priority over the other workgroups' wavefronts on its SIMD
                 if (t < nj) __builtin_amdgcn_s_setprio(SHYFT_BRENT_PRIO);
 #endif
-                for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j]);
+                for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
 #if SHYFT_BRENT_PRIO > 0
                 __builtin_amdgcn_s_setprio(0);
 #endif
