@@ -193,9 +193,19 @@ __device__ inline void ss_compute_shape_vars(const ss_par& p, uint64_t nnn, uint
     alpha = nu / (p.unit_size * (double)ss_lrint(tot_mean / p.unit_size));
 }
 
-// calculator::step (skaugen.h:151-336); returns the response (outflow, sca, swe) through r_*
-__device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_hours, double T, double prec_mm_h,
-                               ss_state& s, double& r_outflow, double& r_sca, double& r_swe, int32_t& err) {
+// calculator::step (skaugen.h:151-336), split at its one expensive, divergent call -- sca_rel_red on a partial
+// melt (skaugen.h:247) -- so that the kernel can hand those calls of a workgroup to as few wavefronts as possible
+// (as pt_gs_k does with corr_lwc). ss_front runs the step up to that call and says whether it is needed (job
+// arguments u, nnn, nu, alpha); ss_back finishes the step given its result. ss_step = front + call + back.
+struct ss_mid {
+    bool done;  // the early "no snow" return (skaugen.h:166-181): the step is complete
+    bool need;  // sca_rel_red(u, nnn, nu, alpha) is needed
+    uint64_t nnn, u, n;
+    double swe, sca, nu, alpha, lwc, total_storage, snow, rain;
+};
+
+__device__ inline void ss_front(const ss_par& p, double step_in_days, double dt_hours, double T, double prec_mm_h,
+                                ss_state& s, ss_mid& m, double& r_outflow, double& r_sca, double& r_swe) {
     const double snow_tol = 1.0e-10;
     const double unit_size = p.unit_size;
     const double prec = prec_mm_h * dt_hours;
@@ -203,6 +213,8 @@ __device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_h
     s.residual = smin(0.0, prec + s.residual);
     const double snow = T < p.tx ? corr_prec : 0.0;
     const double rain = T < p.tx ? 0.0 : corr_prec;
+    m.done = false;
+    m.need = false;
 
     if (s.sca * s.swe < unit_size && snow < snow_tol) {
         r_outflow = (rain + s.sca * (s.swe + s.free_water) + s.residual) / dt_hours;
@@ -219,6 +231,7 @@ __device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_h
         s.num_units = 0;
         r_sca = 0.0;
         r_swe = 0.0;
+        m.done = true;
         return;
     }
 
@@ -247,7 +260,7 @@ __device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_h
     pot_melt -= new_snow_reduction;
     total_new_snow -= new_snow_reduction;
 
-    uint64_t n = 0;
+    uint64_t n = 0, u = 0;
     if (total_new_snow > unit_size) {  // 1. accumulation
         n = (uint64_t)ss_lrint(total_new_snow / unit_size);
         ss_compute_shape_vars(p, nnn, n, 0, sca, 0.0, alpha, nu);
@@ -256,7 +269,7 @@ __device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_h
         swe = (double)nnn * unit_size;
     }
     if (pot_melt > unit_size) {  // 2. melting
-        uint64_t u = (uint64_t)ss_lrint(pot_melt / unit_size);
+        u = (uint64_t)ss_lrint(pot_melt / unit_size);
         if (nnn < u + 2) {
             nnn = 0;
             alpha = alpha_0;
@@ -265,27 +278,43 @@ __device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_h
             lwc = 0.0;
             sca = 0.0;
         } else {
-            const double rel_red_sca = ss_sca_rel_red(u, nnn, nu, alpha, err);
-            const double sca_scale_factor = 1.0 - rel_red_sca;
-            sca = s.sca * sca_scale_factor;
+            m.need = true;  // sca_rel_red(u, nnn, nu, alpha)
+        }
+    }
+    m.nnn = nnn; m.u = u; m.n = n;
+    m.swe = swe; m.sca = sca; m.nu = nu; m.alpha = alpha; m.lwc = lwc;
+    m.total_storage = total_storage; m.snow = snow; m.rain = rain;
+}
+
+__device__ inline void ss_back(const ss_par& p, double dt_hours, ss_state& s, const ss_mid& m, double rel_red_sca,
+                               double& r_outflow, double& r_sca, double& r_swe) {
+    if (m.done) return;
+    const double unit_size = p.unit_size;
+    const double alpha_0 = p.alpha_0;
+    uint64_t nnn = m.nnn, u = m.u;
+    const uint64_t n = m.n;
+    double swe = m.swe, sca = m.sca, nu = m.nu, alpha = m.alpha, lwc = m.lwc;
+    const double total_storage = m.total_storage, snow = m.snow, rain = m.rain;
+    if (m.need) {  // 2. melting, the partial-melt branch (skaugen.h:246-275)
+        const double sca_scale_factor = 1.0 - rel_red_sca;
+        sca = s.sca * sca_scale_factor;
+        swe = (double)(nnn - u) / sca_scale_factor * unit_size;
+        if (swe >= (double)nnn * unit_size) {
+            u = (uint64_t)((long)((double)nnn * rel_red_sca) + 1);
             swe = (double)(nnn - u) / sca_scale_factor * unit_size;
-            if (swe >= (double)nnn * unit_size) {
-                u = (uint64_t)((long)((double)nnn * rel_red_sca) + 1);
-                swe = (double)(nnn - u) / sca_scale_factor * unit_size;
-                if (nnn == u) sca = 0.0;
-            }
-            if (sca < 0.005) {
-                nnn = 0;
-                alpha = alpha_0;
-                nu = alpha_0 * unit_size;
-                swe = 0.0;
-                lwc = 0.0;
-                sca = 0.0;
-            } else {
-                ss_compute_shape_vars(p, nnn, n, u, sca, rel_red_sca, alpha, nu);
-                nnn = (uint64_t)ss_lrint(swe / unit_size);
-                swe = (double)nnn * unit_size;
-            }
+            if (nnn == u) sca = 0.0;
+        }
+        if (sca < 0.005) {
+            nnn = 0;
+            alpha = alpha_0;
+            nu = alpha_0 * unit_size;
+            swe = 0.0;
+            lwc = 0.0;
+            sca = 0.0;
+        } else {
+            ss_compute_shape_vars(p, nnn, n, u, sca, rel_red_sca, alpha, nu);
+            nnn = (uint64_t)ss_lrint(swe / unit_size);
+            swe = (double)nnn * unit_size;
         }
     }
     // 3. lwc from the swe*sca change
@@ -320,6 +349,14 @@ __device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_h
     s.swe = swe;
     s.free_water = lwc;
     s.num_units = nnn;
+}
+
+__device__ inline void ss_step(const ss_par& p, double step_in_days, double dt_hours, double T, double prec_mm_h,
+                               ss_state& s, double& r_outflow, double& r_sca, double& r_swe, int32_t& err) {
+    ss_mid m;
+    ss_front(p, step_in_days, dt_hours, T, prec_mm_h, s, m, r_outflow, r_sca, r_swe);
+    const double rel = m.need ? ss_sca_rel_red(m.u, m.nnn, m.nu, m.alpha, err) : 0.0;
+    ss_back(p, dt_hours, s, m, rel, r_outflow, r_sca, r_swe);
 }
 
 }  // namespace shyft_dev

@@ -33,15 +33,38 @@ constexpr int BLOCK = 256;
 #define SHYFT_PTSSK_OCC
 #endif
 
+// sca_rel_red compaction (COMPACT): a partial melt calls statistics::sca_rel_red (skaugen.h:57-82: a 2-bit
+// Brent, a bracket walk, a 10-bit bisection and two incomplete-gamma cdfs) for 2-50 % of the cells of a melt-season
+// step, scattered over the wavefronts. Each step the workgroup queues its lanes' calls in LDS and the first
+// ceil(jobs/64) wavefronts evaluate them, one per lane; every lane then finishes its step with its own result
+// (the same function of the same arguments: bit-identical to the per-lane call).
+#ifndef SHYFT_PTSSK_COMPACT
+#define SHYFT_PTSSK_COMPACT 1
+#endif
+#ifndef SHYFT_PTSSK_PRIO
+#define SHYFT_PTSSK_PRIO 3  // measured: 135.3 -> 134.5 ms per chunk
+#endif
+
+template <bool COMPACT>
 __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const ptssk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= a.n_cells) return;
-    if (a.active && !a.active[cell]) return;
+    bool valid = cell < a.n_cells;
+    if (valid && a.active && !a.active[cell]) valid = false;
+    if (!COMPACT && !valid) return;
+    const int lc = valid ? cell : 0;  // idle lanes of a COMPACT block compute on cell 0 and store nothing
     const size_t N = (size_t)a.n_cells;
     // forcing column: the lane itself, or the shared cell of a parameter-ensemble lane
     const size_t NF = a.fcol ? (size_t)a.f_cols : N;
-    const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * PTSSK_NP;
+    const size_t fcl = a.fcol ? (size_t)a.fcol[lc] : (size_t)lc;
+    const double* __restrict__ P = a.params + (size_t)a.set_ix[lc] * PTSSK_NP;
+    __shared__ uint64_t ju[BLOCK], jn[BLOCK];
+    __shared__ double jnu[BLOCK], jal[BLOCK], jres[BLOCK];
+    __shared__ int32_t jerr[BLOCK];
+    __shared__ int jcount[2];
+    if (COMPACT) {
+        if (threadIdx.x == 0) jcount[0] = 0;
+        __syncthreads();
+    }
 
     ss_par sp;
     sp.alpha_0 = P[SK_ALPHA0];
@@ -59,25 +82,25 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     const double gm_routed = 1 - gm_direct;
 
     const double* __restrict__ cc = a.cellc;  // pt_ss_k.h:237-245 (same rows as pt_gs_k)
-    const double glacier_fraction = cc[PC_GLACIER * N + cell];
-    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + cell];
-    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + cell];
-    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + cell];
-    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + cell];
-    const double cell_area_m2 = cc[PC_AREA * N + cell];
-    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + cell];
+    const double glacier_fraction = cc[PC_GLACIER * N + lc];
+    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
+    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
+    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + lc];
+    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + lc];
+    const double cell_area_m2 = cc[PC_AREA * N + lc];
+    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
     const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
 
     double* __restrict__ st = a.state;
     ss_state s;
-    s.nu = st[SS_NU * N + cell];
-    s.alpha = st[SS_ALPHA * N + cell];
-    s.sca = st[SS_SCA * N + cell];
-    s.swe = st[SS_SWE * N + cell];
-    s.free_water = st[SS_FREE_WATER * N + cell];
-    s.residual = st[SS_RESIDUAL * N + cell];
-    s.num_units = (uint64_t)st[SS_NUM_UNITS * N + cell];
-    double q = st[SS_KIRCHNER_Q * N + cell];
+    s.nu = st[SS_NU * N + lc];
+    s.alpha = st[SS_ALPHA * N + lc];
+    s.sca = st[SS_SCA * N + lc];
+    s.swe = st[SS_SWE * N + lc];
+    s.free_water = st[SS_FREE_WATER * N + lc];
+    s.residual = st[SS_RESIDUAL * N + lc];
+    s.num_units = (uint64_t)st[SS_NUM_UNITS * N + lc];
+    double q = st[SS_KIRCHNER_Q * N + lc];
     int32_t err = 0;
 
     const size_t TW = (size_t)a.win_len;
@@ -114,9 +137,44 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
         const double rad = f_rad[ff];
         const double rel_hum = f_rh[ff];
         const double prec = f_prec[ff] * p_corr;
-        if (SS) collect_state(wi);
-        double snow_outflow, snow_sca, snow_swe;
-        ss_step(sp, a.step_in_days, a.dt_hours, temp, prec, s, snow_outflow, snow_sca, snow_swe, err);
+        if (SS && valid) collect_state(wi);
+        double snow_outflow = 0, snow_sca = 0, snow_swe = 0;
+        ss_mid m;
+        ss_front(sp, a.step_in_days, a.dt_hours, temp, prec, s, m, snow_outflow, snow_sca, snow_swe);
+        if (!valid) m.need = false;
+        double rel = 0.0;
+        if (COMPACT) {
+            if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (as in the pt_gs_k kernel)
+            int slot = -1;
+            if (m.need) {
+                slot = atomicAdd(&jcount[i & 1], 1);
+                ju[slot] = m.u; jn[slot] = m.nnn; jnu[slot] = m.nu; jal[slot] = m.alpha;
+            }
+            __syncthreads();
+            const int nj = jcount[i & 1];
+            if (nj > 0) {
+#if SHYFT_PTSSK_PRIO > 0
+                if ((int)threadIdx.x < nj) __builtin_amdgcn_s_setprio(SHYFT_PTSSK_PRIO);  // the workgroup's critical path
+#endif
+                for (int j = threadIdx.x; j < nj; j += BLOCK) {
+                    int32_t e = 0;
+                    jres[j] = ss_sca_rel_red(ju[j], jn[j], jnu[j], jal[j], e);
+                    jerr[j] = e;
+                }
+#if SHYFT_PTSSK_PRIO > 0
+                __builtin_amdgcn_s_setprio(0);
+#endif
+                __syncthreads();
+                if (slot >= 0) {
+                    rel = jres[slot];
+                    if (jerr[slot]) err = jerr[slot];
+                }
+            }
+        } else if (m.need) {
+            rel = ss_sca_rel_red(m.u, m.nnn, m.nu, m.alpha, err);
+        }
+        if (!valid) continue;
+        ss_back(sp, a.dt_hours, s, m, rel, snow_outflow, snow_sca, snow_swe);
         // glacier_melt::step (glacier_melt.h:47-52) on the post-step snow covered area
         const double sca_area = cell_area_m2 * s.sca;
         double gm_melt_m3s = 0.0;
@@ -149,6 +207,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
         }
         if (SS && i + 1 == i_end) collect_state(wi + 1);
     }
+    if (!valid) return;
     st[SS_NU * N + cell] = s.nu;
     st[SS_ALPHA * N + cell] = s.alpha;
     st[SS_SCA * N + cell] = s.sca;
@@ -165,6 +224,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptssk_run_kernel, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (SHYFT_PTSSK_COMPACT) hipLaunchKernelGGL(ptssk_run_kernel<true>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    else hipLaunchKernelGGL(ptssk_run_kernel<false>, dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }
