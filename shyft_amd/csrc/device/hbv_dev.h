@@ -23,30 +23,38 @@ constexpr int MB = HBV_MAX_BINS;
 constexpr int MB = HBV_MB_OVERRIDE;
 #endif
 
+// The functions below are templates on the register capacity NB of the bin arrays (deduced from the arrays):
+// HBV_MAX_BINS in general, 5 for the kernel variant that serves parameter sets of at most 5 bins (the
+// reference's default distribution): 2 x 3 fewer state doubles in registers, and the per-bin loops are shorter.
+
 // a[idx] for a runtime idx over a register array. Written as a bit-mask OR so the
 // compiler cannot fold it back into a dynamically indexed (scratch) access, which it
 // does with an equivalent chain of selects. Exact: one mask is all-ones.
-__device__ __forceinline__ double hsel(const double (&a)[MB], int idx) {
+template <int NB>
+__device__ __forceinline__ double hsel(const double (&a)[NB], int idx) {
     unsigned long long v = 0;
 #pragma unroll
-    for (int i = 0; i < MB; ++i) v |= (unsigned long long)__double_as_longlong(a[i]) & (0ULL - (unsigned long long)(idx == i));
+    for (int i = 0; i < NB; ++i) v |= (unsigned long long)__double_as_longlong(a[i]) & (0ULL - (unsigned long long)(idx == i));
     return __longlong_as_double((long long)v);
 }
 
-struct hbv_snow_par {
+template <int NB>
+struct hbv_snow_par_t {
     int nb;
-    double s[MB], I[MB];
+    double s[NB], I[NB];
     double tx, cx, ts, lw, cfr;
 };
+using hbv_snow_par = hbv_snow_par_t<MB>;
 
 // hbv_snow_common::integrate (hbv_snow_common.h:14-44) for a = 0 (every call in
 // the stack integrates from 0)
-__device__ __forceinline__ double hbv_integrate0(const double (&f)[MB], const double (&x)[MB], int n, double b,
+template <int NB>
+__device__ __forceinline__ double hbv_integrate0(const double (&f)[NB], const double (&x)[NB], int n, double b,
                                                  bool f_b_is_zero) {
     const double a = 0.0;
     int left = 0;
 #pragma unroll
-    for (int i = 0; i < MB; ++i)  // while (a > x[left]) ++left;
+    for (int i = 0; i < NB; ++i)  // while (a > x[left]) ++left;
         if (i < n && left == i && a > x[i]) left = i + 1;
     double f_l;
     if (fabs(a - hsel(x, left)) > 1.0e-8 && left > 0) {
@@ -59,7 +67,7 @@ __device__ __forceinline__ double hbv_integrate0(const double (&f)[MB], const do
     double area = 0.0, x_l = a;
     bool done = false;
 #pragma unroll
-    for (int i = 0; i < MB - 1; ++i) {
+    for (int i = 0; i < NB - 1; ++i) {
         if (!done && i >= left && i < n - 1) {
             if (b >= x[i + 1]) {
                 area += 0.5 * (f_l + f[i + 1]) * (x[i + 1] - x_l);
@@ -78,23 +86,24 @@ __device__ __forceinline__ double hbv_integrate0(const double (&f)[MB], const do
 }
 
 // hbv_snow::state::distribute -> distribute_snow (hbv_snow.h:95-99, hbv_snow_common.h:47-66)
-__device__ inline void hbv_distribute(const hbv_snow_par& p, double (&sp)[MB], double (&sw)[MB], double& swe,
+template <int NB>
+__device__ inline void hbv_distribute(const hbv_snow_par_t<NB>& p, double (&sp)[NB], double (&sw)[NB], double& swe,
                                       double& sca) {
 #pragma unroll
-    for (int i = 0; i < MB; ++i) sp[i] = sw[i] = 0.0;
+    for (int i = 0; i < NB; ++i) sp[i] = sw[i] = 0.0;
     if (swe <= 1.0e-3 || sca <= 1.0e-3) {
         swe = sca = 0.0;
         return;
     }
 #pragma unroll
-    for (int i = 0; i < MB; ++i)
+    for (int i = 0; i < NB; ++i)
         if (i < p.nb) sp[i] = sca < p.I[i] ? 0.0 : p.s[i] * swe;
     const double temp_swe = hbv_integrate0(sp, p.I, p.nb, sca, true);
     if (temp_swe < swe) {
         const double corr1 = swe / temp_swe * p.lw;
         const double corr2 = swe / temp_swe * (1.0 - p.lw);
 #pragma unroll
-        for (int i = 0; i < MB; ++i)
+        for (int i = 0; i < NB; ++i)
             if (i < p.nb) {
                 sw[i] = corr1 * sp[i];
                 sp[i] *= corr2;
@@ -103,7 +112,8 @@ __device__ inline void hbv_distribute(const hbv_snow_par& p, double (&sp)[MB], d
 }
 
 // hbv_snow::calculator::step (hbv_snow.h:195-272); returns the outflow in mm/h
-__device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], double (&sw)[MB], double& s_swe,
+template <int NB>
+__device__ inline double hbv_snow_step(const hbv_snow_par_t<NB>& p, double (&sp)[NB], double (&sw)[NB], double& s_swe,
                                        double& s_sca, double step_in_days, double dt_hours, double prec_mm_h,
                                        double temp, int32_t& err) {
     double swe = s_swe;
@@ -122,7 +132,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], 
     swe += snow + sca * rain;
     if (swe < 0.1) {
 #pragma unroll
-        for (int i = 0; i < MB; ++i) sp[i] = sw[i] = 0.0;
+        for (int i = 0; i < NB; ++i) sp[i] = sw[i] = 0.0;
         s_swe = 0.0;
         s_sca = 0.0;
         return total_water / dt_hours;
@@ -130,7 +140,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], 
     if (snow > 0.0) {
         int idx = nb - 1;  // sca_index (hbv_snow.h:175-180)
 #pragma unroll
-        for (int i = MB - 2; i >= 0; --i)
+        for (int i = NB - 2; i >= 0; --i)
             if (i < nb - 1 && sca >= p.I[i] && sca < p.I[i + 1]) idx = i;
         if (sca > 1.0e-5 && sca < 1.0 - 1.0e-5) {
             double f;
@@ -143,19 +153,19 @@ __device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], 
             // sp[idx] *= f, sw[idx] *= f as a multiply of every bin by f or 1.0 (x * 1.0 == x
             // exactly): the compiler turns a guarded per-bin update back into a scratch access
 #pragma unroll
-            for (int i = 0; i < MB; ++i) {
+            for (int i = 0; i < NB; ++i) {
                 const double fi = (i == idx) ? f : 1.0;
                 sp[i] *= fi;
                 sw[i] *= fi;
             }
         }
 #pragma unroll
-        for (int i = 0; i < MB; ++i)
+        for (int i = 0; i < NB; ++i)
             if (i < nb) sp[i] += snow * p.s[i];
         sca = p.I[1];  // at least one bin filled after snowfall
         bool found = false;
 #pragma unroll
-        for (int i = MB - 2; i > 0; --i)
+        for (int i = NB - 2; i > 0; --i)
             if (!found && i <= nb - 2 && p.s[i] > 0.0) {
                 sca = p.I[i + 1];
                 found = true;
@@ -166,7 +176,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], 
     if (potmelt < 0.0) {
         potmelt *= p.cfr;
 #pragma unroll
-        for (int i = 0; i < MB; ++i)  // refreeze (hbv_snow.h:146-158)
+        for (int i = 0; i < NB; ++i)  // refreeze (hbv_snow.h:146-158)
             if (i < nb && sp[i] > 0.0) {
                 if (sw[i] + rain > -potmelt) {
                     sp[i] -= potmelt;
@@ -180,7 +190,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], 
     } else {
         int idx = nb;  // melt_index (hbv_snow.h:182-187)
 #pragma unroll
-        for (int i = MB - 1; i >= 0; --i)
+        for (int i = NB - 1; i >= 0; --i)
             if (i < nb && sp[i] < potmelt) idx = i;
         if (idx == 0) sca = 0.0;
         else if (idx == nb) sca = 1.0;
@@ -190,7 +200,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par& p, double (&sp)[MB], 
             else sca = (1.0 - potmelt / spm) * (sca - Im) + Im;
         }
 #pragma unroll
-        for (int i = 0; i < MB; ++i)  // update_state (hbv_snow.h:160-168)
+        for (int i = 0; i < NB; ++i)  // update_state (hbv_snow.h:160-168)
             if (i < nb) {
                 if (sp[i] > potmelt) {
                     sw[i] += potmelt + rain;

@@ -49,6 +49,7 @@ struct hbv_kargs {
     const uint8_t* active;   // [N] or null
     int32_t* err;            // [N]
     int uniform_params;      // 1: every cell uses parameter set 0 (n_sets == 1)
+    int nb_max;              // the largest snow bin count of the parameter sets
 };
 
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream);

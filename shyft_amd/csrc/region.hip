@@ -1049,6 +1049,11 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.active = h->active.empty() ? nullptr : h->d_active.p;
         a.err = h->d_err.p;
         a.uniform_params = h->n_sets == 1 ? 1 : 0;
+        a.nb_max = 0;
+        for (size_t k = 0; k < h->n_sets; ++k) {
+            const int nb = int(h->params[k * HBV_NP + HK_NB]);
+            if (nb > a.nb_max) a.nb_max = nb;
+        }
         hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
         hip_check(launch_hbv_run(a, h->stream), "hbv_run_kernel launch");
         hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
