@@ -44,7 +44,7 @@ constexpr int BLOCK = 256;
 // wave-uniform and lives in SGPRs instead of 2 x 8 + 15 per-lane doubles of VGPRs
 // NB: register capacity of the bin arrays (HBV_MAX_BINS, or 5 when every parameter set has at most 5 bins and
 // no state series is collected: 10.9 -> 9.4 ms per 512K-cell chunk). Bins NB..HBV_MAX_BINS-1 of the state in
-// HBM are then left as they were, or zeroed when the state is redistributed, as the full kernel does.
+// HBM are then written as zeros, as the oracle's state vector (nb entries, padded) reads back.
 template <bool UNIFORM, int NB>
 __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
@@ -87,18 +87,18 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     double swe = st[HS_SWE * N + cell], sca = st[HS_SCA * N + cell];
     double sm = st[HS_SM * N + cell], uz = st[HS_UZ * N + cell], lz = st[HS_LZ * N + cell];
     double nb_state = st[HS_NB * N + cell];
+    // the state holds nb_state bins (the reference's vectors); the rest read as zero, as the oracle's padding
+    const int nbs = (int)nb_state;
     double sp[NB], sw[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        sp[i] = st[(HS_SP0 + i) * N + cell];
-        sw[i] = st[(HS_SW0 + i) * N + cell];
+        sp[i] = i < nbs ? st[(HS_SP0 + i) * N + cell] : 0.0;
+        sw[i] = i < nbs ? st[(HS_SW0 + i) * N + cell] : 0.0;
     }
     // state.snow.distribute(parameter.snow, false) (hbv_stack.h:310): only on a bin-count mismatch
-    bool redistributed = false;
     if ((int)nb_state != sp_par.nb) {
         hbv_distribute(sp_par, sp, sw, swe, sca);
         nb_state = (double)sp_par.nb;
-        redistributed = true;
     }
     int32_t err = 0;
 
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         st[(HS_SP0 + i) * N + cell] = sp[i];
         st[(HS_SW0 + i) * N + cell] = sw[i];
     }
-    if (NB < HBV_MAX_BINS && redistributed) {
+    if (NB < HBV_MAX_BINS) {
         for (int i = NB; i < HBV_MAX_BINS; ++i) st[(HS_SP0 + i) * N + cell] = st[(HS_SW0 + i) * N + cell] = 0.0;
     }
     if (err) a.err[cell] = err;

@@ -88,13 +88,15 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHPSK_OCC void pthpsk_run_kernel(cons
     double* __restrict__ st = a.state;
     double swe = st[PPS_SWE * N + cell], sca = st[PPS_SCA * N + cell], surface_heat = st[PPS_SURFACE_HEAT * N + cell];
     double nb_state = st[PPS_NB * N + cell];
+    // the state holds nb_state bins (the reference's vectors); the rest read as zero, as the oracle's padding
+    const int nbs = (int)nb_state;
     double sp[MB], sw[MB], alb[MB], iso[MB];
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-        sp[i] = st[(PPS_SP0 + i) * N + cell];
-        sw[i] = st[(PPS_SW0 + i) * N + cell];
-        alb[i] = st[(PPS_ALB0 + i) * N + cell];
-        iso[i] = st[(PPS_ISO0 + i) * N + cell];
+        sp[i] = i < nbs ? st[(PPS_SP0 + i) * N + cell] : 0.0;
+        sw[i] = i < nbs ? st[(PPS_SW0 + i) * N + cell] : 0.0;
+        alb[i] = i < nbs ? st[(PPS_ALB0 + i) * N + cell] : 0.0;
+        iso[i] = i < nbs ? st[(PPS_ISO0 + i) * N + cell] : 0.0;
     }
     double q = st[PPS_KIRCHNER_Q * N + cell];
     // state.hps.distribute(parameter.hps, false) (pt_hps_k.h:236, hbv_physical_snow.h:156-164): only on a

@@ -75,11 +75,13 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const 
     double* __restrict__ st = a.state;
     double swe = st[PHS_SWE * N + cell], sca = st[PHS_SCA * N + cell];
     double nb_state = st[PHS_NB * N + cell];
+    // the state holds nb_state bins (the reference's vectors); the rest read as zero, as the oracle's padding
+    const int nbs = (int)nb_state;
     double sp[MB], sw[MB];
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-        sp[i] = st[(PHS_SP0 + i) * N + cell];
-        sw[i] = st[(PHS_SW0 + i) * N + cell];
+        sp[i] = i < nbs ? st[(PHS_SP0 + i) * N + cell] : 0.0;
+        sw[i] = i < nbs ? st[(PHS_SW0 + i) * N + cell] : 0.0;
     }
     double q = st[PHS_KIRCHNER_Q * N + cell];
     // state.snow.distribute(parameter.hs, false) (pt_hs_k.h:230): only on a bin-count mismatch

@@ -91,6 +91,29 @@ def test_hbv_custom_distribution_two_sets_bitexact(s1, i1, predistributed):
 
 
 @pytest.mark.gpu
+def test_hbv_five_bin_kernel_keeps_and_clears_upper_bins_like_the_oracle():
+    """One parameter set with the default 5 bins and no state series runs the 5-bin kernel instance: state bins 5..7
+    must come out as the oracle's padded state vector: zero, whether the bins were redistributed or kept."""
+    n, T = 300, 24 * 30
+    geo, f = _case(n, T, step0=24 * 60, seed=5)
+    p = synthetic.default_hbv_parameters()
+    st = synthetic.default_hbv_state(n)
+    st[:, 0], st[:, 1] = 40.0, 0.9
+    st[::3, 5] = 8.0                    # claims 8 bins: redistributed to 5, bins 5..7 cleared
+    st[::3, 6:22] = 2.5
+    st[1::3, 0:2] = 0.0                 # snow-free, 5 distributed (empty) bins kept; stale bins 5..7
+    st[1::3, 5] = 5.0
+    st[1::3, 6:22] = 0.0
+    st[1::3, 11:14] = st[1::3, 19:22] = 1.5
+    ref = engines.run_hbv("oracle", geo, p, st, synthetic.T0_2015_US, HOUR, f)
+    got = engines.run_hbv("hip", geo, p, st, synthetic.T0_2015_US, HOUR, f)
+    _assert_same(got, ref, ["full", "state"])
+    assert (got["state"][:, [11, 12, 13, 19, 20, 21]] == 0.0).all()
+    got8 = engines.run_hbv("hip", geo, p, st, synthetic.T0_2015_US, HOUR, f, collect_state=True)  # 8-bin instance
+    _assert_same(got8, ref, ["full", "state"])
+
+
+@pytest.mark.gpu
 def test_hbv_stepwise_equals_full_on_gpu():
     from shyft_amd.region import HipRegion, HBV_STACK, COLLECT_ALL
     n, T = 256, 24 * 10

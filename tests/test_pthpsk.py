@@ -186,3 +186,21 @@ def test_pthpsk_stepwise_equals_full_on_gpu():
         assert np.array_equal(r.get_state(), full["state"])
     finally:
         r.close()
+
+
+@pytest.mark.gpu
+def test_pthpsk_stale_bins_beyond_the_state_count_read_as_zero():
+    """Slots nb..7 of the sp, sw, albedo and iso_pot_energy rows are padding and come back 0 (pthpsk.hpp state)."""
+    n, T = 150, 24 * 20
+    geo, f = _case(n, T, step0=24 * 60, seed=4)
+    st = synthetic.default_pthpsk_state(n, q=2.0)
+    st[:, 0:2] = 0.0
+    st[:, 3] = 5.0
+    st[:, 4:36] = 0.0
+    stale = [c for b in (4, 12, 20, 28) for c in range(b + 5, b + 8)]
+    st[:, stale] = 1.5
+    args = (geo, synthetic.default_pthpsk_parameters(), st, synthetic.T0_2015_US, HOUR, f)
+    ref = engines.run_pthpsk("oracle", *args)
+    got = engines.run_pthpsk("hip", *args)
+    _assert_same(got, ref, ["full", "state"])
+    assert (got["state"][:, stale] == 0.0).all()

@@ -180,3 +180,20 @@ def test_pthsk_stepwise_equals_full_on_gpu():
         assert np.array_equal(r.get_state(), full["state"])
     finally:
         r.close()
+
+
+@pytest.mark.gpu
+def test_pthsk_stale_bins_beyond_the_state_count_read_as_zero():
+    """The state carries nb bins (the reference's vectors); slots nb..7 of the flat row are padding and come back 0."""
+    n, T = 150, 24 * 20
+    geo, f = _case(n, T, step0=24 * 60, seed=4)
+    st = synthetic.default_pthsk_state(n, q=2.0)
+    st[:, 0:2] = 0.0
+    st[:, 2] = 5.0
+    st[:, 3:19] = 0.0
+    st[:, 8:11] = st[:, 16:19] = 1.5
+    args = (geo, synthetic.default_pthsk_parameters(), st, synthetic.T0_2015_US, HOUR, f)
+    ref = engines.run_pthsk("oracle", *args)
+    got = engines.run_pthsk("hip", *args)
+    _assert_same(got, ref, ["full", "state"])
+    assert (got["state"][:, [8, 9, 10, 16, 17, 18]] == 0.0).all()
