@@ -59,6 +59,12 @@ constexpr int BLOCK = SHYFT_BLOCK;
 // the parameter row is then wave-uniform and lives in SGPRs (scalar loads), which frees the VGPRs the
 // per-lane copies would take in the register-bound time loop.
 // ENS: a parameter-ensemble launch (lanes = cells x members): forcing is read from the shared column fcol[lane].
+// SHYFT_PTGSK_LDSC: the 11 per-cell constants in LDS (22 KB per workgroup, 38.9 KB with the job queue: 4
+// workgroups = 16 waves per CU still fit the 160 KB) instead of VGPRs live across the Brent phase. Scratch
+// 400 -> 320 B/lane; 124.8 -> 119.1 ms per 1M-cell chunk over the bench year, bit-exact.
+#ifndef SHYFT_PTGSK_LDSC
+#define SHYFT_PTGSK_LDSC 1
+#endif
 template <bool COMPACT, bool UNIFORM, bool ENS = false>
 __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
@@ -78,6 +84,39 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     gcell.altitude = cc[PC_ALTITUDE * N + lc];
     gcell.cv2 = cc[PC_CV2 * N + lc];
     gcell.inv_cv2 = cc[PC_INV_CV2 * N + lc];
+#if SHYFT_PTGSK_LDSC
+    // the cell constants live in LDS, not in VGPRs: each use reloads its lane's slot (the barriers of the
+    // step keep the compiler from hoisting the loads), so none of them is live across the Brent phase
+    __shared__ double lcc[11][BLOCK];
+    {
+        const int t = threadIdx.x;
+        lcc[0][t] = gcell.forest_fraction;
+        lcc[1][t] = gcell.altitude;
+        lcc[2][t] = gcell.cv2;
+        lcc[3][t] = gcell.inv_cv2;
+        lcc[4][t] = cc[PC_GLACIER * N + lc];
+        lcc[5][t] = cc[PC_SNOW_STORAGE * N + lc];
+        lcc[6][t] = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
+        lcc[7][t] = cc[PC_DIRECT_RESPONSE * N + lc];
+        lcc[8][t] = cc[PC_KIRCHNER_FRACTION * N + lc];
+        lcc[9][t] = cc[PC_AREA * N + lc];
+        lcc[10][t] = cc[PC_GLACIER_AREA * N + lc];
+    }
+#define glacier_fraction (lcc[4][threadIdx.x])
+#define snow_storage_fraction (lcc[5][threadIdx.x])
+#define kirchner_routed_prec (lcc[6][threadIdx.x])
+#define direct_response_fraction (lcc[7][threadIdx.x])
+#define kirchner_fraction (lcc[8][threadIdx.x])
+#define cell_area_m2 (lcc[9][threadIdx.x])
+#define glacier_area_m2 (lcc[10][threadIdx.x])
+#define LOAD_GCELL()                                   \
+    do {                                               \
+        gcell.forest_fraction = lcc[0][threadIdx.x];   \
+        gcell.altitude = lcc[1][threadIdx.x];          \
+        gcell.cv2 = lcc[2][threadIdx.x];               \
+        gcell.inv_cv2 = lcc[3][threadIdx.x];           \
+    } while (0)
+#else
     const double glacier_fraction = cc[PC_GLACIER * N + lc];
     const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
     const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
@@ -85,6 +124,8 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + lc];
     const double cell_area_m2 = cc[PC_AREA * N + lc];
     const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
+#define LOAD_GCELL() ((void)0)
+#endif
 
     const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
 
@@ -166,6 +207,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
         gs_mid m;
         m.need = false;
         m.done = true;
+        LOAD_GCELL();
         if (valid)
             gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc, carry);
         PROF_MARK(0);  // forcing + gs_front
@@ -225,6 +267,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
         PROF_MARK(2);  // Brent phase
         if (!valid) continue;
         double gs_sca, gs_storage, gs_outflow;
+        LOAD_GCELL();
         gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc, carry);
         PROF_MARK(3);  // gs_back
 
@@ -275,6 +318,16 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     st[PS_KIRCHNER_Q * N + cell] = q;
     if (err) a.err[cell] = err;
 }
+#undef LOAD_GCELL
+#if SHYFT_PTGSK_LDSC
+#undef glacier_fraction
+#undef snow_storage_fraction
+#undef kirchner_routed_prec
+#undef direct_response_fraction
+#undef kirchner_fraction
+#undef cell_area_m2
+#undef glacier_area_m2
+#endif
 
 }  // namespace
 
