@@ -71,6 +71,8 @@ struct ptssk_kargs {
     double* state_series;    // [PTSSK_NSC][win_len+1][N] or null
     const uint8_t* active;   // [N] or null
     int32_t* err;            // [N]
+    int uniform_params;      // 1: every cell uses parameter set 0 (n_sets == 1)
+    int nb_max;              // pt_hs_k: the largest snow bin count of the parameter sets
 };
 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream);

@@ -28,12 +28,16 @@ constexpr int BLOCK = 256;
 #ifndef SHYFT_PTHSK_WAVES
 #define SHYFT_PTHSK_WAVES 3  // measured: compiler choice (1) 123 ms, 2: 70, 3: 64, 4: 70 per 730-step chunk
 #endif
-#if SHYFT_PTHSK_WAVES > 0
-#define SHYFT_PTHSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHSK_WAVES, SHYFT_PTHSK_WAVES)))
-#else
-#define SHYFT_PTHSK_OCC
+#ifndef SHYFT_PTHSK_WAVES_U
+#define SHYFT_PTHSK_WAVES_U 4  // the uniform-parameter instance; measured (5 bins): 2: 69.2, 3: 55.3, 4: 50.6 ms per chunk
 #endif
+#define SHYFT_PTHSK_W (UNIFORM ? SHYFT_PTHSK_WAVES_U : SHYFT_PTHSK_WAVES)
+#define SHYFT_PTHSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHSK_W, SHYFT_PTHSK_W)))
 
+// UNIFORM: every cell uses parameter set 0 (the row, incl. the bin distribution, in SGPRs instead of VGPRs).
+// NB: register capacity of the snow bins, HBV_MAX_BINS or 5 (as in the hbv_stack kernel: one parameter set of at
+// most 5 bins and no state series; bins NB..7 of the state are written as 0, the oracle's padding).
+template <bool UNIFORM, int NB>
 __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const pthsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
@@ -42,12 +46,12 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const 
     // forcing column: the lane itself, or the shared cell of a parameter-ensemble lane
     const size_t NF = a.fcol ? (size_t)a.f_cols : N;
     const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * PTHSK_NP;
+    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * PTHSK_NP;
 
-    hbv_snow_par sp_par;
+    hbv_snow_par_t<NB> sp_par;
     sp_par.nb = (int)P[PH_NB];
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
+    for (int i = 0; i < NB; ++i) {
         sp_par.s[i] = P[PH_S0 + i];
         sp_par.I[i] = P[PH_I0 + i];
     }
@@ -77,9 +81,9 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const 
     double nb_state = st[PHS_NB * N + cell];
     // the state holds nb_state bins (the reference's vectors); the rest read as zero, as the oracle's padding
     const int nbs = (int)nb_state;
-    double sp[MB], sw[MB];
+    double sp[NB], sw[NB];
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
+    for (int i = 0; i < NB; ++i) {
         sp[i] = i < nbs ? st[(PHS_SP0 + i) * N + cell] : 0.0;
         sw[i] = i < nbs ? st[(PHS_SW0 + i) * N + cell] : 0.0;
     }
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const 
         SS[PHC_SCA * SSS + o] = sca;
         SS[PHC_SWE * SSS + o] = swe * snow_storage_fraction;
 #pragma unroll
-        for (int i = 0; i < MB; ++i) {
+        for (int i = 0; i < NB; ++i) {
             SS[(PHC_SP0 + i) * SSS + o] = sp[i];
             SS[(PHC_SW0 + i) * SSS + o] = sw[i];
         }
@@ -164,9 +168,12 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const 
     st[PHS_SCA * N + cell] = sca;
     st[PHS_NB * N + cell] = nb_state;
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
+    for (int i = 0; i < NB; ++i) {
         st[(PHS_SP0 + i) * N + cell] = sp[i];
         st[(PHS_SW0 + i) * N + cell] = sw[i];
+    }
+    if (NB < HBV_MAX_BINS) {
+        for (int i = NB; i < HBV_MAX_BINS; ++i) st[(PHS_SP0 + i) * N + cell] = st[(PHS_SW0 + i) * N + cell] = 0.0;
     }
     st[PHS_KIRCHNER_Q * N + cell] = q;
     if (err) a.err[cell] = err;
@@ -177,6 +184,11 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const 
 hipError_t launch_pthsk_run(const pthsk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(pthsk_run_kernel, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
+        hipLaunchKernelGGL((pthsk_run_kernel<true, 5>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.uniform_params)
+        hipLaunchKernelGGL((pthsk_run_kernel<true, HBV_MAX_BINS>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else
+        hipLaunchKernelGGL((pthsk_run_kernel<false, HBV_MAX_BINS>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

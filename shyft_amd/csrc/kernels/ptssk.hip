@@ -45,7 +45,15 @@ constexpr int BLOCK = 256;
 #define SHYFT_PTSSK_PRIO 3  // measured: 135.3 -> 134.5 ms per chunk
 #endif
 
-template <bool COMPACT>
+// SHYFT_PTSSK_LDSC: the 7 per-cell constants in LDS (14 KB per workgroup next to the 11 KB job queue) instead
+// of VGPRs live across the sca_rel_red phase (as in the pt_gs_k kernel).
+#ifndef SHYFT_PTSSK_LDSC
+#define SHYFT_PTSSK_LDSC 1
+#endif
+
+// UNIFORM: every cell uses parameter set 0, so the parameter row is wave-uniform (SGPRs, not 18 per-lane
+// doubles held in VGPRs for the whole launch)
+template <bool COMPACT, bool UNIFORM>
 __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const ptssk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
@@ -56,7 +64,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     // forcing column: the lane itself, or the shared cell of a parameter-ensemble lane
     const size_t NF = a.fcol ? (size_t)a.f_cols : N;
     const size_t fcl = a.fcol ? (size_t)a.fcol[lc] : (size_t)lc;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[lc] * PTSSK_NP;
+    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[lc] * PTSSK_NP;
     __shared__ uint64_t ju[BLOCK], jn[BLOCK];
     __shared__ double jnu[BLOCK], jal[BLOCK], jres[BLOCK];
     __shared__ int32_t jerr[BLOCK];
@@ -82,6 +90,26 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     const double gm_routed = 1 - gm_direct;
 
     const double* __restrict__ cc = a.cellc;  // pt_ss_k.h:237-245 (same rows as pt_gs_k)
+#if SHYFT_PTSSK_LDSC
+    __shared__ double lcc[7][BLOCK];
+    {
+        const int t = threadIdx.x;
+        lcc[0][t] = cc[PC_GLACIER * N + lc];
+        lcc[1][t] = cc[PC_SNOW_STORAGE * N + lc];
+        lcc[2][t] = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
+        lcc[3][t] = cc[PC_DIRECT_RESPONSE * N + lc];
+        lcc[4][t] = cc[PC_KIRCHNER_FRACTION * N + lc];
+        lcc[5][t] = cc[PC_AREA * N + lc];
+        lcc[6][t] = cc[PC_GLACIER_AREA * N + lc];
+    }
+#define glacier_fraction (lcc[0][threadIdx.x])
+#define snow_storage_fraction (lcc[1][threadIdx.x])
+#define kirchner_routed_prec (lcc[2][threadIdx.x])
+#define direct_response_fraction (lcc[3][threadIdx.x])
+#define kirchner_fraction (lcc[4][threadIdx.x])
+#define cell_area_m2 (lcc[5][threadIdx.x])
+#define glacier_area_m2 (lcc[6][threadIdx.x])
+#else
     const double glacier_fraction = cc[PC_GLACIER * N + lc];
     const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
     const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
@@ -89,6 +117,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + lc];
     const double cell_area_m2 = cc[PC_AREA * N + lc];
     const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
+#endif
     const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
 
     double* __restrict__ st = a.state;
@@ -218,13 +247,23 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     st[SS_KIRCHNER_Q * N + cell] = q;
     if (err) a.err[cell] = err;
 }
+#if SHYFT_PTSSK_LDSC
+#undef glacier_fraction
+#undef snow_storage_fraction
+#undef kirchner_routed_prec
+#undef direct_response_fraction
+#undef kirchner_fraction
+#undef cell_area_m2
+#undef glacier_area_m2
+#endif
 
 }  // namespace
 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (SHYFT_PTSSK_COMPACT) hipLaunchKernelGGL(ptssk_run_kernel<true>, dim3(grid), dim3(BLOCK), 0, stream, a);
-    else hipLaunchKernelGGL(ptssk_run_kernel<false>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (!SHYFT_PTSSK_COMPACT) hipLaunchKernelGGL((ptssk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.uniform_params) hipLaunchKernelGGL((ptssk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else hipLaunchKernelGGL((ptssk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

@@ -1016,6 +1016,12 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
         a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
         a.active = h->active.empty() ? nullptr : h->d_active.p;
         a.err = h->d_err.p;
+        a.uniform_params = h->n_sets == 1 ? 1 : 0;
+        a.nb_max = HBV_MAX_BINS;
+        if (h->pthsk()) {
+            a.nb_max = 0;
+            for (size_t k = 0; k < h->n_sets; ++k) a.nb_max = std::max(a.nb_max, int(h->params[k * PTHSK_NP + PH_NB]));
+        }
         hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
         if (h->pthpsk())
             hip_check(launch_pthpsk_run(a, h->stream), "pthpsk_run_kernel launch");
