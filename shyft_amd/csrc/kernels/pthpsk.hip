@@ -28,12 +28,14 @@ constexpr int BLOCK = 256;
 #ifndef SHYFT_PTHPSK_WAVES
 #define SHYFT_PTHPSK_WAVES 2  // measured: compiler choice (1) 151 ms, 2: 91, 3: 123
 #endif
-#if SHYFT_PTHPSK_WAVES > 0
-#define SHYFT_PTHPSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHPSK_WAVES, SHYFT_PTHPSK_WAVES)))
-#else
-#define SHYFT_PTHPSK_OCC
+#ifndef SHYFT_PTHPSK_WAVES_U
+#define SHYFT_PTHPSK_WAVES_U 3  // the uniform-parameter instance; measured: 2: 93.4, 3: 85.0 ms per chunk (per-lane rows at 2: 91.0)
 #endif
+#define SHYFT_PTHPSK_W (UNIFORM ? SHYFT_PTHPSK_WAVES_U : SHYFT_PTHPSK_WAVES)
+#define SHYFT_PTHPSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHPSK_W, SHYFT_PTHPSK_W)))
 
+// UNIFORM: every cell uses parameter set 0 (the parameter row wave-uniform, in SGPRs instead of VGPRs)
+template <bool UNIFORM>
 __global__ __launch_bounds__(BLOCK) SHYFT_PTHPSK_OCC void pthpsk_run_kernel(const pthpsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
@@ -41,7 +43,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHPSK_OCC void pthpsk_run_kernel(cons
     const size_t N = (size_t)a.n_cells;
     const size_t NF = a.fcol ? (size_t)a.f_cols : N;
     const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
-    const double* __restrict__ P = a.params + (size_t)a.set_ix[cell] * PTHPSK_NP;
+    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * PTHPSK_NP;
 
     const double dt_us = a.dt_us;
     const double dts = dt_us / 1e6;  // to_seconds(dt)
@@ -214,6 +216,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTHPSK_OCC void pthpsk_run_kernel(cons
 hipError_t launch_pthpsk_run(const pthpsk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(pthpsk_run_kernel, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (a.uniform_params) hipLaunchKernelGGL((pthpsk_run_kernel<true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else hipLaunchKernelGGL((pthpsk_run_kernel<false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }
