@@ -45,6 +45,18 @@ constexpr int BLOCK = 256;
 // NB: register capacity of the bin arrays (HBV_MAX_BINS, or 5 when every parameter set has at most 5 bins and
 // no state series is collected: 10.9 -> 9.4 ms per 512K-cell chunk). Bins NB..HBV_MAX_BINS-1 of the state in
 // HBM are then written as zeros, as the oracle's state vector (nb entries, padded) reads back.
+// streaming hints for the read-once forcing and write-once responses (variant builds: -DSHYFT_HBV_NT=1)
+#ifndef SHYFT_HBV_NT
+#define SHYFT_HBV_NT 0
+#endif
+#if SHYFT_HBV_NT
+#define HBV_LD(p) __builtin_nontemporal_load(&(p))
+#define HBV_ST(p, v) __builtin_nontemporal_store((v), &(p))
+#else
+#define HBV_LD(p) (p)
+#define HBV_ST(p, v) ((p) = (v))
+#endif
+
 template <bool UNIFORM, int NB>
 __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
@@ -137,7 +149,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         rt[k] = rr[k] = rh[k] = rp[k] = 0.0;
         if (a.step0 + k < i_end) {
             const size_t ff = (size_t)(a.step0 + k - a.win0) * NF + fcl;
-            rt[k] = f_temp[ff]; rr[k] = f_rad[ff]; rh[k] = f_rh[ff]; rp[k] = f_prec[ff];
+            rt[k] = HBV_LD(f_temp[ff]); rr[k] = HBV_LD(f_rad[ff]); rh[k] = HBV_LD(f_rh[ff]); rp[k] = HBV_LD(f_prec[ff]);
         }
     }
     for (int i = a.step0; i < i_end; ++i) {
@@ -150,7 +162,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         }
         if (i + D < i_end) {
             const size_t fn = (wi + D) * NF + fcl;
-            rt[D - 1] = f_temp[fn]; rr[D - 1] = f_rad[fn]; rh[D - 1] = f_rh[fn]; rp[D - 1] = f_prec[fn];
+            rt[D - 1] = HBV_LD(f_temp[fn]); rr[D - 1] = HBV_LD(f_rad[fn]); rh[D - 1] = HBV_LD(f_rh[fn]); rp[D - 1] = HBV_LD(f_prec[fn]);
         }
         const double prec = prec_raw * p_corr;
         if (SS) collect_state(wi);
@@ -186,8 +198,8 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         const double charge_m3s = +(cell_area_m2 * prec * mmh_to_m3s_scale_factor) -
                                   (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
-        R[HR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
-        R[HR_CHARGE_M3S * RS + fo] = charge_m3s;
+        HBV_ST(R[HR_AVG_DISCHARGE * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        HBV_ST(R[HR_CHARGE_M3S * RS + fo], charge_m3s);
         if (a.collect >= 1) {
             // response.snow.snow_state is never written by hbv_snow::step (hbv_snow.h:121-124): the
             // reference collects its default (swe = sca = 0)
