@@ -85,6 +85,15 @@ __device__ inline double gs_calc_q(double a, double b, double z, double lga) {
     return a * b * g.p1 + z * (1.0 - g.p);
 }
 
+// the same with every elementary function inlined (the Brent solver's f, SHYFT_BRENT_INL)
+__device__ __forceinline__ double gs_calc_q_inl(double a, double b, double z, double lga) {
+    const gamma_p_result g = gamma_p_prefix_inl(a, z / b, lga, detmath::gamma_snow_policy_eps(a));
+    return a * b * g.p1 + z * (1.0 - g.p);
+}
+#ifndef SHYFT_BRENT_INL
+#define SHYFT_BRENT_INL 1
+#endif
+
 // corr_lwc (gamma_snow.h:214-227): boost brent_find_minima over [0, z1],
 // 12 bits, 60 iterations; golden constant is the float literal 0.3819660f.
 #ifdef SHYFT_PROF
@@ -106,7 +115,11 @@ __device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, doub
 #ifdef SHYFT_PROF
         ++nf_evals;
 #endif
+#if SHYFT_BRENT_INL
+        const double v = gs_calc_q_inl(a2, b2, z, lga2) - Q1;
+#else
         const double v = gs_calc_q(a2, b2, z, lga2) - Q1;
+#endif
         return v * v;
     };
     double min = 0.0, max = z1;

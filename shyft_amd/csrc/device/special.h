@@ -60,6 +60,12 @@ struct dev_math {
     __device__ static double log(double x) { return dlog(x); }
 };
 using gamma_p_result = detmath::gamma_pq_result;
+// the same functions forced inline: for leaf solvers (the Brent job of gamma_snow), where an out-of-line call would
+// cost its ABI entry wait (s_waitcnt on every outstanding memory operation) in the middle of a dependent chain
+struct dev_math_inl {
+    __device__ static __forceinline__ double exp(double x) { return detmath::exp(x); }
+    __device__ static __forceinline__ double log(double x) { return detmath::log(x); }
+};
 
 // lga = lgamma(a) supplied by the caller (shape changes rarely, so callers cache it);
 // eps = the relative termination tolerance (boost precision policy of the caller)
@@ -68,6 +74,10 @@ __device__ SHYFT_INL_GP gamma_p_result gamma_p_prefix(double a, double x, double
     gamma_p_result r; r.p = 0.5; r.p1 = 0.4; r.prefix = 0.01; return r;  // timing ablation only (wrong results)
 #endif
     return detmath::gamma_pq<dev_math>(a, x, lga, eps);
+}
+
+__device__ __forceinline__ gamma_p_result gamma_p_prefix_inl(double a, double x, double lga, double eps) {
+    return detmath::gamma_pq<dev_math_inl>(a, x, lga, eps);
 }
 
 // gamma_snow's calls: boost precision policy by shape (gamma_snow.h:195-197)

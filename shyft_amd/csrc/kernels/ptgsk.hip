@@ -163,7 +163,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
     __shared__ double jz1[BLOCK], ja1[BLOCK], jb1[BLOCK], ja2[BLOCK], jb2[BLOCK], jq1[BLOCK], jlg2[BLOCK], jres[BLOCK];
     __shared__ int jcount[2];
     if (COMPACT) {
-        if (threadIdx.x == 0) jcount[0] = 0;
+        if (threadIdx.x == 0) jcount[0] = jcount[1] = 0;  // both: the first step may be odd (start_step)
         __syncthreads();
     }
 

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     __shared__ int32_t jerr[BLOCK];
     __shared__ int jcount[2];
     if (COMPACT) {
-        if (threadIdx.x == 0) jcount[0] = 0;
+        if (threadIdx.x == 0) jcount[0] = jcount[1] = 0;  // both: the first step may be odd (start_step)
         __syncthreads();
     }
 

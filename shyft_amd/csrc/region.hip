@@ -201,6 +201,14 @@ int fail(shyft_hip_region* h, const std::string& msg) {
     return 1;
 }
 
+// host <-> region copies are ordered on the region's stream (created non-blocking, so a null-stream copy would
+// not wait for a run or copy_state still queued there) and complete before returning, like hipMemcpy
+hipError_t region_copy(shyft_hip_region* h, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, h->stream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(h->stream);
+}
+
 template <class F>
 int guarded(shyft_hip_region* h, F&& f) {
     try {
@@ -241,8 +249,8 @@ void update_ix_to_id_mapping(shyft_hip_region* h) {
     for (size_t i = 0; i < h->n; ++i) cells[pos[h->cix[i]]++] = int32_t(i);
     h->d_seg_cells.alloc(h->n);
     h->d_seg_off.alloc(C + 1);
-    hip_check(hipMemcpy(h->d_seg_cells.p, cells.data(), h->n * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
-    hip_check(hipMemcpy(h->d_seg_off.p, off.data(), (C + 1) * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
+    hip_check(region_copy(h, h->d_seg_cells.p, cells.data(), h->n * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
+    hip_check(region_copy(h, h->d_seg_off.p, off.data(), (C + 1) * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
 }
 
 // derived per-set parameter rows and per-cell constants (pt_gs_k.h:347-357,
@@ -265,10 +273,10 @@ void update_derived_hbv(shyft_hip_region* h) {
     h->d_params.alloc(h->params.size());
     h->d_cellc.alloc(cc.size());
     h->d_set_ix.alloc(N);
-    hip_check(hipMemcpy(h->d_params.p, h->params.data(), h->params.size() * sizeof(double), hipMemcpyHostToDevice),
+    hip_check(region_copy(h, h->d_params.p, h->params.data(), h->params.size() * sizeof(double), hipMemcpyHostToDevice),
               "upload params");
-    hip_check(hipMemcpy(h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
-    hip_check(hipMemcpy(h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
+    hip_check(region_copy(h, h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
+    hip_check(region_copy(h, h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
     h->derived_dirty = false;
 }
 
@@ -298,10 +306,10 @@ void update_derived_ptssk(shyft_hip_region* h) {
     h->d_params.alloc(h->params.size());
     h->d_cellc.alloc(cc.size());
     h->d_set_ix.alloc(N);
-    hip_check(hipMemcpy(h->d_params.p, h->params.data(), h->params.size() * sizeof(double), hipMemcpyHostToDevice),
+    hip_check(region_copy(h, h->d_params.p, h->params.data(), h->params.size() * sizeof(double), hipMemcpyHostToDevice),
               "upload params");
-    hip_check(hipMemcpy(h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
-    hip_check(hipMemcpy(h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
+    hip_check(region_copy(h, h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
+    hip_check(region_copy(h, h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
     h->derived_dirty = false;
 }
 
@@ -354,9 +362,9 @@ void update_derived(shyft_hip_region* h) {
     h->d_params.alloc(P.size());
     h->d_cellc.alloc(cc.size());
     h->d_set_ix.alloc(N);
-    hip_check(hipMemcpy(h->d_params.p, P.data(), P.size() * sizeof(double), hipMemcpyHostToDevice), "upload params");
-    hip_check(hipMemcpy(h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
-    hip_check(hipMemcpy(h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
+    hip_check(region_copy(h, h->d_params.p, P.data(), P.size() * sizeof(double), hipMemcpyHostToDevice), "upload params");
+    hip_check(region_copy(h, h->d_cellc.p, cc.data(), cc.size() * sizeof(double), hipMemcpyHostToDevice), "upload cellc");
+    hip_check(region_copy(h, h->d_set_ix.p, h->set_ix.data(), N * sizeof(int32_t), hipMemcpyHostToDevice), "upload set_ix");
     h->derived_dirty = false;
 }
 
@@ -523,7 +531,7 @@ int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* r
         std::vector<double> z(h->n);
         for (size_t i = 0; i < h->n; ++i) z[i] = h->geo[i * 11 + 2];
         h->d_alt.alloc(h->n);
-        hip_check(hipMemcpy(h->d_alt.p, z.data(), h->n * sizeof(double), hipMemcpyHostToDevice), "upload z");
+        hip_check(region_copy(h, h->d_alt.p, z.data(), h->n * sizeof(double), hipMemcpyHostToDevice), "upload z");
         h->has_geo = true;
         h->derived_dirty = true;
         h->dst_dirty = true;
@@ -611,8 +619,8 @@ int shyft_hip_set_time_axis(shyft_hip_region* h, int64_t t0_us, int64_t dt_us, s
         }
         h->d_doy.alloc(n_steps);
         h->d_trel.alloc(n_steps);
-        hip_check(hipMemcpy(h->d_doy.p, doy.data(), n_steps * sizeof(int32_t), hipMemcpyHostToDevice), "upload doy");
-        hip_check(hipMemcpy(h->d_trel.p, trel.data(), n_steps * sizeof(int64_t), hipMemcpyHostToDevice), "upload trel");
+        hip_check(region_copy(h, h->d_doy.p, doy.data(), n_steps * sizeof(int32_t), hipMemcpyHostToDevice), "upload doy");
+        hip_check(region_copy(h, h->d_trel.p, trel.data(), n_steps * sizeof(int64_t), hipMemcpyHostToDevice), "upload trel");
         alloc_window(h);
         h->derived_dirty = true;
     });
@@ -675,7 +683,7 @@ int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, siz
         h->active.assign(h->n, 0);
         for (size_t i = 0; i < h->n; ++i) h->active[i] = cf[h->cix[i]] ? 1 : 0;
         h->d_active.alloc(h->n);
-        hip_check(hipMemcpy(h->d_active.p, h->active.data(), h->n, hipMemcpyHostToDevice), "upload filter");
+        hip_check(region_copy(h, h->d_active.p, h->active.data(), h->n, hipMemcpyHostToDevice), "upload filter");
     });
 }
 
@@ -687,7 +695,7 @@ int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_field
         std::vector<double> soa(n_fields * N);
         for (size_t i = 0; i < N; ++i)
             for (size_t f = 0; f < n_fields; ++f) soa[f * N + i] = state[i * n_fields + f];
-        hip_check(hipMemcpy(h->d_state.p, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice), "upload state");
+        hip_check(region_copy(h, h->d_state.p, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice), "upload state");
         h->has_state = true;
     });
 }
@@ -705,9 +713,15 @@ int shyft_hip_copy_state(shyft_hip_region* dst, const shyft_hip_region* src) {
                                  hipMemcpyDeviceToDevice, dst->stream), "copy_state");
         // anything later queued on the source stream (a run, set_state's upload) must not overwrite the source
         // state while the destination stream still reads it
+        // (set_state / get_state copy on the region stream too, region_copy). The event lives on the source
+        // region's device; a copy between two devices completes before returning instead.
         shyft_hip_region* s = const_cast<shyft_hip_region*>(src);
-        hip_check(hipEventRecord(s->ev_copy, dst->stream), "copy_state: record");
-        hip_check(hipStreamWaitEvent(s->stream, s->ev_copy, 0), "copy_state: order source stream");
+        if (src->device == dst->device) {
+            hip_check(hipEventRecord(s->ev_copy, dst->stream), "copy_state: record");
+            hip_check(hipStreamWaitEvent(s->stream, s->ev_copy, 0), "copy_state: order source stream");
+        } else {
+            hip_check(hipStreamSynchronize(dst->stream), "copy_state: cross-device copy");
+        }
         dst->has_state = true;
     });
 }
@@ -719,7 +733,7 @@ int shyft_hip_get_state(const shyft_hip_region* hc, double* state, size_t n_fiel
         if (n_fields != h->n_state_fields()) throw std::runtime_error("get_state: wrong number of state fields");
         const size_t N = h->n;
         std::vector<double> soa(n_fields * N);
-        hip_check(hipMemcpy(soa.data(), h->d_state.p, soa.size() * sizeof(double), hipMemcpyDeviceToHost), "download state");
+        hip_check(region_copy(h, soa.data(), h->d_state.p, soa.size() * sizeof(double), hipMemcpyDeviceToHost), "download state");
         for (size_t i = 0; i < N; ++i)
             for (size_t f = 0; f < n_fields; ++f) state[i * n_fields + f] = soa[f * N + i];
     });
@@ -794,8 +808,8 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
             }
             h->d_dst_xyz.alloc(3 * N);
             h->d_slope.alloc(N);
-            hip_check(hipMemcpy(h->d_dst_xyz.p, xyz.data(), 3 * N * sizeof(double), hipMemcpyHostToDevice), "upload dst");
-            hip_check(hipMemcpy(h->d_slope.p, slope.data(), N * sizeof(double), hipMemcpyHostToDevice), "upload slope");
+            hip_check(region_copy(h, h->d_dst_xyz.p, xyz.data(), 3 * N * sizeof(double), hipMemcpyHostToDevice), "upload dst");
+            hip_check(region_copy(h, h->d_slope.p, slope.data(), N * sizeof(double), hipMemcpyHostToDevice), "upload slope");
             h->dst_dirty = false;
         }
         auto& tab = h->idw[var];
@@ -898,11 +912,11 @@ int shyft_hip_interpolate_btk(shyft_hip_region* h, size_t n_sources, const doubl
         const bool all = D == N;
         if (xyz != h->btk_xyz_host || index != h->btk_index_host || h->btk_dst_version == 0) {
             h->d_btk_xyz.alloc(3 * D);
-            hip_check(hipMemcpy(h->d_btk_xyz.p, xyz.data(), 3 * D * sizeof(double), hipMemcpyHostToDevice),
+            hip_check(region_copy(h, h->d_btk_xyz.p, xyz.data(), 3 * D * sizeof(double), hipMemcpyHostToDevice),
                       "upload btk destinations");
             if (!all) {
                 h->d_btk_index.alloc(D);
-                hip_check(hipMemcpy(h->d_btk_index.p, index.data(), D * sizeof(int32_t), hipMemcpyHostToDevice),
+                hip_check(region_copy(h, h->d_btk_index.p, index.data(), D * sizeof(int32_t), hipMemcpyHostToDevice),
                           "upload btk index");
             }
             h->btk_xyz_host.swap(xyz);
@@ -1112,8 +1126,9 @@ static void finish_run(shyft_hip_region* h) {
     if (first == none) return;
     const size_t i = size_t(first);
     int32_t code = 0;
-    hip_check(hipMemcpy(&code, h->d_err.p + i, sizeof(int32_t), hipMemcpyDeviceToHost), "download err");
-    hip_check(hipMemset(h->d_err.p, 0, h->n * sizeof(int32_t)), "memset");
+    hip_check(region_copy(h, &code, h->d_err.p + i, sizeof(int32_t), hipMemcpyDeviceToHost), "download err");
+    hip_check(hipMemsetAsync(h->d_err.p, 0, h->n * sizeof(int32_t), h->stream), "memset");
+    hip_check(hipStreamSynchronize(h->stream), "memset");
     if (code == ERR_NEGATIVE_OUTFLOW)
         throw std::runtime_error("Negative outflow: total_water - swe < -1e-6 in hbv_snow (cell " + std::to_string(i) + ")");
     if (code == ERR_SKAUGEN_BISECT)
@@ -1204,7 +1219,7 @@ int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* 
             return;
         }
         h->d_sel.alloc(std::max(h->d_sel.n, sel.size()));
-        hip_check(hipMemcpy(h->d_sel.p, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload sel");
+        hip_check(region_copy(h, h->d_sel.p, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload sel");
         double sum_area = 0.0;
         const double* w = nullptr;
         if (weighted) {
@@ -1214,7 +1229,7 @@ int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* 
                 sum_area += a[k];
             }
             h->d_w.alloc(std::max(h->d_w.n, a.size()));
-            hip_check(hipMemcpy(h->d_w.p, a.data(), a.size() * sizeof(double), hipMemcpyHostToDevice), "upload w");
+            hip_check(region_copy(h, h->d_w.p, a.data(), a.size() * sizeof(double), hipMemcpyHostToDevice), "upload w");
             w = h->d_w.p;
         }
         h->d_tmp.alloc(std::max(h->d_tmp.n, n));
@@ -1367,9 +1382,9 @@ int shyft_hip_set_routing_groups(shyft_hip_region* h, const int32_t* group_of_ce
             if (group_of_cell[i] >= 0) cells[size_t(pos[size_t(group_of_cell[i])]++)] = int32_t(i);
         h->d_rseg_off.alloc(n_groups + 1);
         h->d_rseg_cells.alloc(std::max<size_t>(1, cells.size()));
-        hip_check(hipMemcpy(h->d_rseg_off.p, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
+        hip_check(region_copy(h, h->d_rseg_off.p, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
         if (!cells.empty())
-            hip_check(hipMemcpy(h->d_rseg_cells.p, cells.data(), cells.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+            hip_check(region_copy(h, h->d_rseg_cells.p, cells.data(), cells.size() * sizeof(int32_t), hipMemcpyHostToDevice),
                       "upload");
         h->n_route_groups = n_groups;
     });

@@ -118,3 +118,59 @@ def test_stepwise_equals_full_run():
         r.close()
     _assert_bitexact(outs[1][0], outs[0][0], "discharge")
     _assert_bitexact(outs[1][1], outs[0][1], "state")
+
+
+def test_odd_start_step_and_single_steps_in_snowfall_bitexact():
+    """run_cells from an ODD start_step and one step at a time, in January (Brent jobs on most steps): the
+    workgroup's double-buffered job counter must start at zero for either parity of the first step."""
+    n, T = 300, 24 * 6
+    geo, f, params, state = _region(n, T)
+    cpu = engines.run("oracle", geo, params, state, synthetic.T0_2015_US, HOUR, f, 37, 61, full=True)
+    gpu = engines.run("hip", geo, params, state, synthetic.T0_2015_US, HOUR, f, 37, 61, full=True)
+    for k in range(8):
+        _assert_bitexact(gpu["full"][k][37:98], cpu["full"][k][37:98], f"series {k}")
+    _assert_bitexact(gpu["state"], cpu["state"], "final state")
+    from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_ALL
+    r = HipRegion(PT_GS_K, n)
+    try:
+        r.set_geo(geo)
+        r.set_parameters(params)
+        r.set_time_axis(synthetic.T0_2015_US, HOUR, T)
+        r.set_collection(COLLECT_ALL)
+        r.set_state(state)
+        for v in range(5):
+            r.set_forcing(v, 0, f[v])
+        for i in range(37, 98):
+            r.run_cells(0, i, 1)
+        got = np.stack([r.get_series(k, 37, 61) for k in range(8)])
+        _assert_bitexact(got, cpu["full"][:, 37:98], "single-step series")
+        _assert_bitexact(r.get_state(), cpu["state"], "single-step final state")
+    finally:
+        r.close()
+
+
+def test_copy_state_then_set_state_on_source():
+    """copy_state(dst, src) followed at once by set_state(src): the destination keeps the source's old state
+    (the upload is ordered after the copy on the region streams)."""
+    from shyft_amd.region import HipRegion, PT_GS_K
+    n = 1 << 16
+    geo, f, params, state = _region(n, 4)
+    regs = [HipRegion(PT_GS_K, n) for _ in range(2)]
+    try:
+        for r in regs:
+            r.set_geo(geo)
+            r.set_parameters(params)
+        src, dst = regs
+        a = state.copy()
+        a[:, 1] = np.arange(n) * 1e-3  # lwc
+        b = state.copy()
+        b[:, 1] = -1.0
+        for _ in range(3):
+            src.set_state(a)
+            dst.copy_state_from(src)
+            src.set_state(b)
+            _assert_bitexact(dst.get_state(), a, "destination state")
+            _assert_bitexact(src.get_state(), b, "source state")
+    finally:
+        for r in regs:
+            r.close()

@@ -101,3 +101,39 @@ def test_ptssk_ragged_parameter_sets_and_stepwise():
     ref = engines.run_ptssk("oracle", geo, params, st, synthetic.T0_2015_US, HOUR, f, 48, 100, set_ix=ix)
     got = engines.run_ptssk("hip", geo, params, st, synthetic.T0_2015_US, HOUR, f, 48, 100, set_ix=ix)
     _assert_same(ref, got, ("full", "state"))
+
+
+@pytest.mark.gpu
+def test_ptssk_odd_start_step_and_single_steps_in_melt():
+    """run_cells from an ODD start_step and one step at a time in April (partial melts queue sca_rel_red
+    jobs): the double-buffered job counter starts at zero for either parity of the first step."""
+    n, T = 300, 24 * 4
+    step0 = 24 * 100
+    geo, f = _case(n, T, step0=step0, seed=11)
+    st = synthetic.default_ptssk_state(n)
+    p = synthetic.default_ptssk_parameters()
+    # a snow pack to melt: run the oracle through the winter first
+    geo_w, f_w = _case(n, step0, seed=11)
+    st = oracle_lib.ptssk_run(geo_w, p, st, synthetic.T0_2015_US, HOUR, f_w, full=False)["state"]
+    t0 = synthetic.T0_2015_US + step0 * HOUR
+    ref = engines.run_ptssk("oracle", geo, p, st, t0, HOUR, f, 13, 59, collect_state=False)
+    got = engines.run_ptssk("hip", geo, p, st, t0, HOUR, f, 13, 59, collect_state=False)
+    assert np.array_equal(ref["full"][:, 13:72], got["full"][:, 13:72])
+    assert np.array_equal(ref["state"], got["state"])
+    from shyft_amd.region import HipRegion, PT_SS_K, COLLECT_ALL
+    r = HipRegion(PT_SS_K, n)
+    try:
+        r.set_geo(geo)
+        r.set_parameters(np.atleast_2d(p))
+        r.set_time_axis(t0, HOUR, T)
+        r.set_collection(COLLECT_ALL)
+        r.set_state(st)
+        for v in range(5):
+            r.set_forcing(v, 0, f[v])
+        for i in range(13, 72):
+            r.run_cells(0, i, 1)
+        s = np.stack([r.get_series(k, 13, 59) for k in range(8)])
+        assert np.array_equal(s, ref["full"][:, 13:72])
+        assert np.array_equal(r.get_state(), ref["state"])
+    finally:
+        r.close()
