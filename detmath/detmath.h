@@ -356,6 +356,57 @@ DM_FN void gamma_series_sums(double a, double x, double eps, double& B_out, doub
     E_out = E;
 }
 
+// gamma_series_sums in blocks of GPQ_BLOCK terms: every term of a block is computed before any of the block's exit
+// tests is looked at, so a block is straight-line code (its chains of E, B and x^n run side by side instead of one
+// branch per term); the state is then taken at the first term whose test fires -- the term at which the loop above
+// breaks -- so the result is the loop's, bit for bit. A block in which the 2^-200 rescale would fire before the exit,
+// and the last terms before the 2000 cap, run the plain loop from the block's start.
+#ifndef GPQ_BLOCK
+#define GPQ_BLOCK 8
+#endif
+DM_FN void gamma_series_sums_blk(double a, double x, double eps, double& B_out, double& E_out) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    double ap = a, E = 1.0, B = 0.0, xn = 1.0;
+    int n = 1;
+    while (n + GPQ_BLOCK - 1 <= 2000) {
+        double apk = ap, Ek = E, Bk = B, xk = xn;
+        double rB = 0.0, rE = 0.0;
+        int hit = 0;   // 1: exit test fired (result in rB, rE); 2: rescale needed first (replay this block)
+        #pragma unroll
+        for (int k = 0; k < GPQ_BLOCK; ++k) {
+            apk = apk + 1.0;
+            xk = xk * x;
+            Ek = Ek * apk;
+            Bk = DM_FMA(Bk, apk, xk);
+            const bool stop = xk < eps * (Bk + Ek);
+            const bool big = Ek > GPQ_SCALE_HI;
+            if (hit == 0 && stop) { hit = 1; rB = Bk; rE = Ek; }
+            if (hit == 0 && big) hit = 2;
+        }
+        if (hit == 1) { B_out = rB; E_out = rE; return; }
+        if (hit == 2) break;
+        ap = apk; E = Ek; B = Bk; xn = xk;
+        n += GPQ_BLOCK;
+    }
+    for (; n <= 2000; ++n) {
+        ap = ap + 1.0;
+        xn = xn * x;
+        E = E * ap;
+        B = DM_FMA(B, ap, xn);
+        if (xn < eps * (B + E)) break;
+        if (E > GPQ_SCALE_HI) {
+            DM_NO_SPECULATE();
+            E = E * GPQ_SCALE;
+            B = B * GPQ_SCALE;
+            xn = xn * GPQ_SCALE;
+        }
+    }
+    B_out = B;
+    E_out = E;
+}
+
 // Wallis recurrence for K = b0 + a1/(b1 + a2/(b2 + ...)) = P / Qd
 DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double& Qd_out) {
 #if defined(__clang__)
@@ -372,6 +423,63 @@ DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double&
         const double Pn = DM_FMA(b, P, an * Pm);
         const double Qn = DM_FMA(b, Qd, an * Qm);
         // |Pn/Qn - P/Qd| < eps |Pn/Qn|  <=>  |Pn Qd - P Qn| < eps |Pn Qd|
+        const double cross = Pn * Qd;
+        const double diff = cross - P * Qn;
+        Pm = P; Qm = Qd;
+        P = Pn; Qd = Qn;
+        if (DM_FABS(diff) <= eps * DM_FABS(cross)) break;
+        const double aP = DM_FABS(P);
+        if (aP > GPQ_SCALE_HI) {
+            DM_NO_SPECULATE();
+            P = P * GPQ_SCALE; Qd = Qd * GPQ_SCALE; Pm = Pm * GPQ_SCALE; Qm = Qm * GPQ_SCALE;
+        }
+    }
+    P_out = P;
+    Qd_out = Qd;
+}
+
+// gamma_cf_terms in blocks (as gamma_series_sums_blk): the same terms, the state of the first term whose
+// convergence test fires; a block where the rescale would fire first, and the terms near the cap, run the plain loop.
+DM_FN void gamma_cf_terms_blk(double a, double x, double eps, double& P_out, double& Qd_out) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    double b = x + 1.0 - a;
+    double Pm = 1.0, Qm = 0.0;
+    double P = b, Qd = 1.0;
+    double di = 0.0;
+    int i = 1;
+    while (i + GPQ_BLOCK - 1 <= 2000) {
+        double bk = b, Pmk = Pm, Qmk = Qm, Pk = P, Qk = Qd, dk = di;
+        double rP = 0.0, rQ = 0.0;
+        int hit = 0;
+        #pragma unroll
+        for (int k = 0; k < GPQ_BLOCK; ++k) {
+            dk = dk + 1.0;
+            const double an = -dk * (dk - a);
+            bk = bk + 2.0;
+            const double Pn = DM_FMA(bk, Pk, an * Pmk);
+            const double Qn = DM_FMA(bk, Qk, an * Qmk);
+            const double cross = Pn * Qk;
+            const double diff = cross - Pk * Qn;
+            Pmk = Pk; Qmk = Qk;
+            Pk = Pn; Qk = Qn;
+            const bool stop = DM_FABS(diff) <= eps * DM_FABS(cross);
+            const bool big = DM_FABS(Pk) > GPQ_SCALE_HI;
+            if (hit == 0 && stop) { hit = 1; rP = Pk; rQ = Qk; }
+            if (hit == 0 && big) hit = 2;
+        }
+        if (hit == 1) { P_out = rP; Qd_out = rQ; return; }
+        if (hit == 2) break;
+        b = bk; Pm = Pmk; Qm = Qmk; P = Pk; Qd = Qk; di = dk;
+        i += GPQ_BLOCK;
+    }
+    for (; i <= 2000; ++i) {
+        di = di + 1.0;
+        const double an = -di * (di - a);
+        b = b + 2.0;
+        const double Pn = DM_FMA(b, P, an * Pm);
+        const double Qn = DM_FMA(b, Qd, an * Qm);
         const double cross = Pn * Qd;
         const double diff = cross - P * Qn;
         Pm = P; Qm = Qd;
@@ -427,6 +535,18 @@ DM_FN gamma_pq_result gamma_pq(double a, double x, double lga, double eps = 2.22
     double u, v;
     if (kind == GPQ_SERIES) gamma_series_sums(a, x, eps, u, v);
     else gamma_cf_terms(a, x, eps, u, v);
+    return gamma_pq_finish(kind, a, prefix, u, v);
+}
+
+// gamma_pq with the blocked series / continued fraction: the same result bit for bit (the GPU kernels' choice)
+template <class M>
+DM_FN gamma_pq_result gamma_pq_blk(double a, double x, double lga, double eps = 2.220446049250313e-16) {
+    const int kind = gamma_pq_kind(a, x);
+    if (kind < GPQ_SERIES) return gamma_pq_finish(kind, a, 0.0, 0.0, 0.0);
+    const double prefix = gamma_pq_prefix<M>(a, x, lga);
+    double u, v;
+    if (kind == GPQ_SERIES) gamma_series_sums_blk(a, x, eps, u, v);
+    else gamma_cf_terms_blk(a, x, eps, u, v);
     return gamma_pq_finish(kind, a, prefix, u, v);
 }
 

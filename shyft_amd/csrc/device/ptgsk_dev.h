@@ -91,7 +91,7 @@ __device__ __forceinline__ double gs_calc_q_inl(double a, double b, double z, do
     return a * b * g.p1 + z * (1.0 - g.p);
 }
 #ifndef SHYFT_BRENT_INL
-#define SHYFT_BRENT_INL 1
+#define SHYFT_BRENT_INL 0
 #endif
 
 // corr_lwc (gamma_snow.h:214-227): boost brent_find_minima over [0, z1],

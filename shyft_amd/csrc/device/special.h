@@ -37,6 +37,11 @@ __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b 
 #ifndef SHYFT_INL_GP
 #define SHYFT_INL_GP inline
 #endif
+// SHYFT_GPQ_BLK: the incomplete gamma's series / continued fraction in straight-line blocks of GPQ_BLOCK terms
+// (detmath::gamma_pq_blk, bit-identical to the term-by-term loop the oracle runs)
+#ifndef SHYFT_GPQ_BLK
+#define SHYFT_GPQ_BLK 1
+#endif
 #ifndef SHYFT_DM_INLINE
 #define SHYFT_DM_INLINE __noinline__
 #endif
@@ -73,11 +78,19 @@ __device__ SHYFT_INL_GP gamma_p_result gamma_p_prefix(double a, double x, double
 #ifdef SHYFT_ABLATE_GAMMA
     gamma_p_result r; r.p = 0.5; r.p1 = 0.4; r.prefix = 0.01; return r;  // timing ablation only (wrong results)
 #endif
+#if SHYFT_GPQ_BLK
+    return detmath::gamma_pq_blk<dev_math>(a, x, lga, eps);
+#else
     return detmath::gamma_pq<dev_math>(a, x, lga, eps);
+#endif
 }
 
 __device__ __forceinline__ gamma_p_result gamma_p_prefix_inl(double a, double x, double lga, double eps) {
+#if SHYFT_GPQ_BLK
+    return detmath::gamma_pq_blk<dev_math_inl>(a, x, lga, eps);
+#else
     return detmath::gamma_pq<dev_math_inl>(a, x, lga, eps);
+#endif
 }
 
 // gamma_snow's calls: boost precision policy by shape (gamma_snow.h:195-197)
