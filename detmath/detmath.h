@@ -71,14 +71,20 @@ DM_FN double pow2i(int k) {
 }
 
 // ---------------------------------------------------------------- exp
-// returns exp(x); for |x| inside the finite range the error is < 1 ulp
-DM_FN double exp(double x) {
+// exp(x) = 2^k e^r, x = k ln2 + r (Cody-Waite), e^r by Taylor to r^13 (remainder < 5e-18). For |x| <= 708 the
+// scaling by 2^k (k in [-1021, 1021], e^r in [0.70, 1.42]) is exact, so it is one ldexp; exp_general holds the
+// overflow / underflow / NaN cases (and gives the same value on the fast range, which the tests check).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DM_LDEXP(p, k) __builtin_ldexp((p), (k))
+#define DM_COLD __attribute__((noinline, cold))
+#else
+#define DM_LDEXP(p, k) std::ldexp((p), (k))
+#define DM_COLD
+#endif
+DM_FN double exp_poly(double x, double& kf_out) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
-    if (is_nan(x)) return x;
-    if (x > 709.782712893384) return inf();
-    if (x < -745.1332191019412) return 0.0;
     const double INV_LN2 = 1.4426950408889634;
     const double LN2_HI = 6.93147180369123816490e-01;  // upper 32 bits of ln2
     const double LN2_LO = 1.90821492927058770002e-10;
@@ -102,10 +108,31 @@ DM_FN double exp(double x) {
     p = DM_FMA(p, r, 0.5);
     p = DM_FMA(p, r, 1.0);
     p = DM_FMA(p, r, 1.0);
+    kf_out = kf;
+    return p;
+}
+
+// every x (the reference formulation: NaN, overflow, gradual underflow)
+DM_COLD DM_FN double exp_general(double x) {
+    if (is_nan(x)) return x;
+    if (x > 709.782712893384) return inf();
+    if (x < -745.1332191019412) return 0.0;
+    double kf;
+    const double p = exp_poly(x, kf);
     const int k = (int)kf;
     if (k > 1023) return (p * pow2i(1023)) * pow2i(k - 1023);
     if (k < -1021) return (p * pow2i(k + 1000)) * pow2i(-1000);
     return p * pow2i(k);
+}
+
+// returns exp(x); for |x| inside the finite range the error is < 1 ulp
+DM_FN double exp(double x) {
+    if (DM_FABS(x) <= 708.0) {
+        double kf;
+        const double p = exp_poly(x, kf);
+        return DM_LDEXP(p, (int)kf);
+    }
+    return exp_general(x);
 }
 
 // ---------------------------------------------------------------- log (double-double core)
@@ -164,7 +191,8 @@ DM_FN void log_dd(double x, double& hi, double& lo) {
     lo = small - (hi - sum);
 }
 
-DM_FN double log(double x) {
+// every x (NaN, negative, zero, infinity, subnormal)
+DM_COLD DM_FN double log_general(double x) {
     if (is_nan(x)) return x;
     if (x < 0.0) return qnan();
     if (x == 0.0) return -inf();
@@ -172,6 +200,15 @@ DM_FN double log(double x) {
     double hi, lo;
     log_dd(x, hi, lo);
     return hi;
+}
+
+DM_FN double log(double x) {
+    if (x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308) {  // positive, normal, finite
+        double hi, lo;
+        log_dd(x, hi, lo);  // (its subnormal branch is not taken)
+        return hi;
+    }
+    return log_general(x);
 }
 
 // ---------------------------------------------------------------- pow
@@ -334,63 +371,32 @@ DM_FN double gamma_pq_prefix(double a, double x, double lga) {
 constexpr double GPQ_SCALE_HI = 1.0e200, GPQ_SCALE = 6.2230152778611417e-61;  // 2^-200
 
 // series: E = (a+1)...(a+n), B = sum_{k>=1} x^k E/(a+1..a+k)
+// Blocks of 4 terms first: the four terms and their exit tests are computed before any test is looked at
+// (straight-line code, one branch per block instead of two per term); the block whose test fires returns the
+// state of its FIRST firing term, which is where the term-by-term loop stops. A block in which E passes the
+// rescale threshold is run again term by term (the loop below), so every result is the loop's, bit for bit.
 DM_FN void gamma_series_sums(double a, double x, double eps, double& B_out, double& E_out) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
     double ap = a, E = 1.0, B = 0.0, xn = 1.0;
-    for (int n = 1; n <= 2000; ++n) {
-        ap = ap + 1.0;
-        xn = xn * x;
-        E = E * ap;
-        B = DM_FMA(B, ap, xn);
-        if (xn < eps * (B + E)) break;
-        if (E > GPQ_SCALE_HI) {
-            DM_NO_SPECULATE();
-            E = E * GPQ_SCALE;
-            B = B * GPQ_SCALE;
-            xn = xn * GPQ_SCALE;
+    int n0 = 1;
+    for (; n0 + 3 <= 2000; n0 += 4) {
+        const double a1 = ap + 1.0, x1 = xn * x, E1 = E * a1, B1 = DM_FMA(B, a1, x1);
+        const double a2 = a1 + 1.0, x2 = x1 * x, E2 = E1 * a2, B2 = DM_FMA(B1, a2, x2);
+        const double a3 = a2 + 1.0, x3 = x2 * x, E3 = E2 * a3, B3 = DM_FMA(B2, a3, x3);
+        const double a4 = a3 + 1.0, x4 = x3 * x, E4 = E3 * a4, B4 = DM_FMA(B3, a4, x4);
+        const bool t1 = x1 < eps * (B1 + E1), t2 = x2 < eps * (B2 + E2), t3 = x3 < eps * (B3 + E3),
+                   t4 = x4 < eps * (B4 + E4);
+        if ((E1 > GPQ_SCALE_HI) | (E2 > GPQ_SCALE_HI) | (E3 > GPQ_SCALE_HI) | (E4 > GPQ_SCALE_HI)) break;
+        if (t1 | t2 | t3 | t4) {
+            B_out = t1 ? B1 : t2 ? B2 : t3 ? B3 : B4;
+            E_out = t1 ? E1 : t2 ? E2 : t3 ? E3 : E4;
+            return;
         }
+        ap = a4; xn = x4; E = E4; B = B4;
     }
-    B_out = B;
-    E_out = E;
-}
-
-// gamma_series_sums in blocks of GPQ_BLOCK terms: every term of a block is computed before any of the block's exit
-// tests is looked at, so a block is straight-line code (its chains of E, B and x^n run side by side instead of one
-// branch per term); the state is then taken at the first term whose test fires -- the term at which the loop above
-// breaks -- so the result is the loop's, bit for bit. A block in which the 2^-200 rescale would fire before the exit,
-// and the last terms before the 2000 cap, run the plain loop from the block's start.
-#ifndef GPQ_BLOCK
-#define GPQ_BLOCK 8
-#endif
-DM_FN void gamma_series_sums_blk(double a, double x, double eps, double& B_out, double& E_out) {
-#if defined(__clang__)
-#pragma clang fp contract(off)
-#endif
-    double ap = a, E = 1.0, B = 0.0, xn = 1.0;
-    int n = 1;
-    while (n + GPQ_BLOCK - 1 <= 2000) {
-        double apk = ap, Ek = E, Bk = B, xk = xn;
-        double rB = 0.0, rE = 0.0;
-        int hit = 0;   // 1: exit test fired (result in rB, rE); 2: rescale needed first (replay this block)
-        #pragma unroll
-        for (int k = 0; k < GPQ_BLOCK; ++k) {
-            apk = apk + 1.0;
-            xk = xk * x;
-            Ek = Ek * apk;
-            Bk = DM_FMA(Bk, apk, xk);
-            const bool stop = xk < eps * (Bk + Ek);
-            const bool big = Ek > GPQ_SCALE_HI;
-            if (hit == 0 && stop) { hit = 1; rB = Bk; rE = Ek; }
-            if (hit == 0 && big) hit = 2;
-        }
-        if (hit == 1) { B_out = rB; E_out = rE; return; }
-        if (hit == 2) break;
-        ap = apk; E = Ek; B = Bk; xn = xk;
-        n += GPQ_BLOCK;
-    }
-    for (; n <= 2000; ++n) {
+    for (int n = n0; n <= 2000; ++n) {
         ap = ap + 1.0;
         xn = xn * x;
         E = E * ap;
@@ -408,6 +414,7 @@ DM_FN void gamma_series_sums_blk(double a, double x, double eps, double& B_out, 
 }
 
 // Wallis recurrence for K = b0 + a1/(b1 + a2/(b2 + ...)) = P / Qd
+// (blocks of 2 terms first, as gamma_series_sums)
 DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double& Qd_out) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -416,70 +423,27 @@ DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double&
     double Pm = 1.0, Qm = 0.0;  // n-1
     double P = b, Qd = 1.0;     // n (= 0)
     double di = 0.0;  // i as a double (exact), counted instead of converted each term
-    for (int i = 1; i <= 2000; ++i) {
+    int i0 = 1;
+    for (; i0 + 1 <= 2000; i0 += 2) {
+        const double d1 = di + 1.0, an1 = -d1 * (d1 - a), b1 = b + 2.0;
+        const double P1 = DM_FMA(b1, P, an1 * Pm), Q1 = DM_FMA(b1, Qd, an1 * Qm);
+        const double c1 = P1 * Qd, e1 = c1 - P * Q1;
+        const double d2 = d1 + 1.0, an2 = -d2 * (d2 - a), b2 = b1 + 2.0;
+        const double P2 = DM_FMA(b2, P1, an2 * P), Q2 = DM_FMA(b2, Q1, an2 * Qd);
+        const double c2 = P2 * Q1, e2 = c2 - P1 * Q2;
+        const bool t1 = DM_FABS(e1) <= eps * DM_FABS(c1), t2 = DM_FABS(e2) <= eps * DM_FABS(c2);
+        if (t1) { P_out = P1; Qd_out = Q1; return; }
+        if (DM_FABS(P1) > GPQ_SCALE_HI || DM_FABS(P2) > GPQ_SCALE_HI) break;
+        if (t2) { P_out = P2; Qd_out = Q2; return; }
+        di = d2; b = b2; Pm = P1; Qm = Q1; P = P2; Qd = Q2;
+    }
+    for (int i = i0; i <= 2000; ++i) {
         di = di + 1.0;
         const double an = -di * (di - a);
         b = b + 2.0;
         const double Pn = DM_FMA(b, P, an * Pm);
         const double Qn = DM_FMA(b, Qd, an * Qm);
         // |Pn/Qn - P/Qd| < eps |Pn/Qn|  <=>  |Pn Qd - P Qn| < eps |Pn Qd|
-        const double cross = Pn * Qd;
-        const double diff = cross - P * Qn;
-        Pm = P; Qm = Qd;
-        P = Pn; Qd = Qn;
-        if (DM_FABS(diff) <= eps * DM_FABS(cross)) break;
-        const double aP = DM_FABS(P);
-        if (aP > GPQ_SCALE_HI) {
-            DM_NO_SPECULATE();
-            P = P * GPQ_SCALE; Qd = Qd * GPQ_SCALE; Pm = Pm * GPQ_SCALE; Qm = Qm * GPQ_SCALE;
-        }
-    }
-    P_out = P;
-    Qd_out = Qd;
-}
-
-// gamma_cf_terms in blocks (as gamma_series_sums_blk): the same terms, the state of the first term whose
-// convergence test fires; a block where the rescale would fire first, and the terms near the cap, run the plain loop.
-DM_FN void gamma_cf_terms_blk(double a, double x, double eps, double& P_out, double& Qd_out) {
-#if defined(__clang__)
-#pragma clang fp contract(off)
-#endif
-    double b = x + 1.0 - a;
-    double Pm = 1.0, Qm = 0.0;
-    double P = b, Qd = 1.0;
-    double di = 0.0;
-    int i = 1;
-    while (i + GPQ_BLOCK - 1 <= 2000) {
-        double bk = b, Pmk = Pm, Qmk = Qm, Pk = P, Qk = Qd, dk = di;
-        double rP = 0.0, rQ = 0.0;
-        int hit = 0;
-        #pragma unroll
-        for (int k = 0; k < GPQ_BLOCK; ++k) {
-            dk = dk + 1.0;
-            const double an = -dk * (dk - a);
-            bk = bk + 2.0;
-            const double Pn = DM_FMA(bk, Pk, an * Pmk);
-            const double Qn = DM_FMA(bk, Qk, an * Qmk);
-            const double cross = Pn * Qk;
-            const double diff = cross - Pk * Qn;
-            Pmk = Pk; Qmk = Qk;
-            Pk = Pn; Qk = Qn;
-            const bool stop = DM_FABS(diff) <= eps * DM_FABS(cross);
-            const bool big = DM_FABS(Pk) > GPQ_SCALE_HI;
-            if (hit == 0 && stop) { hit = 1; rP = Pk; rQ = Qk; }
-            if (hit == 0 && big) hit = 2;
-        }
-        if (hit == 1) { P_out = rP; Qd_out = rQ; return; }
-        if (hit == 2) break;
-        b = bk; Pm = Pmk; Qm = Qmk; P = Pk; Qd = Qk; di = dk;
-        i += GPQ_BLOCK;
-    }
-    for (; i <= 2000; ++i) {
-        di = di + 1.0;
-        const double an = -di * (di - a);
-        b = b + 2.0;
-        const double Pn = DM_FMA(b, P, an * Pm);
-        const double Qn = DM_FMA(b, Qd, an * Qm);
         const double cross = Pn * Qd;
         const double diff = cross - P * Qn;
         Pm = P; Qm = Qd;
@@ -535,18 +499,6 @@ DM_FN gamma_pq_result gamma_pq(double a, double x, double lga, double eps = 2.22
     double u, v;
     if (kind == GPQ_SERIES) gamma_series_sums(a, x, eps, u, v);
     else gamma_cf_terms(a, x, eps, u, v);
-    return gamma_pq_finish(kind, a, prefix, u, v);
-}
-
-// gamma_pq with the blocked series / continued fraction: the same result bit for bit (the GPU kernels' choice)
-template <class M>
-DM_FN gamma_pq_result gamma_pq_blk(double a, double x, double lga, double eps = 2.220446049250313e-16) {
-    const int kind = gamma_pq_kind(a, x);
-    if (kind < GPQ_SERIES) return gamma_pq_finish(kind, a, 0.0, 0.0, 0.0);
-    const double prefix = gamma_pq_prefix<M>(a, x, lga);
-    double u, v;
-    if (kind == GPQ_SERIES) gamma_series_sums_blk(a, x, eps, u, v);
-    else gamma_cf_terms_blk(a, x, eps, u, v);
     return gamma_pq_finish(kind, a, prefix, u, v);
 }
 

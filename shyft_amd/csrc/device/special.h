@@ -37,11 +37,6 @@ __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b 
 #ifndef SHYFT_INL_GP
 #define SHYFT_INL_GP inline
 #endif
-// SHYFT_GPQ_BLK: the incomplete gamma's series / continued fraction in straight-line blocks of GPQ_BLOCK terms
-// (detmath::gamma_pq_blk, bit-identical to the term-by-term loop the oracle runs)
-#ifndef SHYFT_GPQ_BLK
-#define SHYFT_GPQ_BLK 1
-#endif
 #ifndef SHYFT_DM_INLINE
 #define SHYFT_DM_INLINE __noinline__
 #endif
@@ -49,7 +44,10 @@ __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b 
 #define SHYFT_DM_INLINE_POW __noinline__
 #endif
 __device__ SHYFT_DM_INLINE double dexp(double x) { return detmath::exp(x); }
-__device__ SHYFT_DM_INLINE double dlog(double x) { return detmath::log(x); }
+#ifndef SHYFT_DM_INLINE_LOG
+#define SHYFT_DM_INLINE_LOG SHYFT_DM_INLINE
+#endif
+__device__ SHYFT_DM_INLINE_LOG double dlog(double x) { return detmath::log(x); }
 __device__ SHYFT_DM_INLINE_POW double dpow(double x, double y) { return detmath::pow(x, y); }
 __device__ __noinline__ double dlgamma(double x) { return detmath::lgamma(x); }
 // structured powers (detmath::pow4 / pow8 / powr, the oracle's OPOW4 / OPOW8 / OPOWR)
@@ -78,19 +76,11 @@ __device__ SHYFT_INL_GP gamma_p_result gamma_p_prefix(double a, double x, double
 #ifdef SHYFT_ABLATE_GAMMA
     gamma_p_result r; r.p = 0.5; r.p1 = 0.4; r.prefix = 0.01; return r;  // timing ablation only (wrong results)
 #endif
-#if SHYFT_GPQ_BLK
-    return detmath::gamma_pq_blk<dev_math>(a, x, lga, eps);
-#else
     return detmath::gamma_pq<dev_math>(a, x, lga, eps);
-#endif
 }
 
 __device__ __forceinline__ gamma_p_result gamma_p_prefix_inl(double a, double x, double lga, double eps) {
-#if SHYFT_GPQ_BLK
-    return detmath::gamma_pq_blk<dev_math_inl>(a, x, lga, eps);
-#else
     return detmath::gamma_pq<dev_math_inl>(a, x, lga, eps);
-#endif
 }
 
 // gamma_snow's calls: boost precision policy by shape (gamma_snow.h:195-197)

@@ -72,8 +72,8 @@ static double mean_cyc(const std::vector<unsigned long long>& c) {
     double s = 0; for (auto v : c) s += (double)v; return s / c.size();
 }
 
-int main() {
-    FILE* f = fopen("tools/mb/jobs_jan.bin", "rb");
+int main(int argc, char** argv) {
+    FILE* f = fopen(argc > 1 ? argv[1] : "tools/mb/jobs_jan.bin", "rb");
     if (!f) { printf("no jobs file\n"); return 1; }
     std::vector<double> h(16384 * 5);
     const int n = (int)(fread(h.data(), sizeof(double), h.size(), f) / 5);

@@ -4,7 +4,7 @@ usage (GPU box): python tools/run_chunks.py [lib.so|-] [cells] [chunks]   ('-' =
 import os
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 if len(sys.argv) > 1 and sys.argv[1] != "-":
     os.environ["SHYFT_HIP_LIB"] = os.path.abspath(sys.argv[1])
 from shyft_amd import synthetic  # noqa: E402
