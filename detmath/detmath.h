@@ -47,6 +47,12 @@
 #pragma clang fp contract(off)
 #endif
 
+// DM_GPQ_BLOCKED: the incomplete gamma's series / continued fraction start with blocks of terms (below); the
+// results are the same either way, so this is a code-shape choice only (register pressure vs branches)
+#ifndef DM_GPQ_BLOCKED
+#define DM_GPQ_BLOCKED 0
+#endif
+
 namespace detmath {
 
 
@@ -76,7 +82,7 @@ DM_FN double pow2i(int k) {
 // overflow / underflow / NaN cases (and gives the same value on the fast range, which the tests check).
 #if defined(__HIP_DEVICE_COMPILE__)
 #define DM_LDEXP(p, k) __builtin_ldexp((p), (k))
-#define DM_COLD __attribute__((noinline, cold))
+#define DM_COLD
 #else
 #define DM_LDEXP(p, k) std::ldexp((p), (k))
 #define DM_COLD
@@ -381,6 +387,7 @@ DM_FN void gamma_series_sums(double a, double x, double eps, double& B_out, doub
 #endif
     double ap = a, E = 1.0, B = 0.0, xn = 1.0;
     int n0 = 1;
+#if DM_GPQ_BLOCKED
     for (; n0 + 3 <= 2000; n0 += 4) {
         const double a1 = ap + 1.0, x1 = xn * x, E1 = E * a1, B1 = DM_FMA(B, a1, x1);
         const double a2 = a1 + 1.0, x2 = x1 * x, E2 = E1 * a2, B2 = DM_FMA(B1, a2, x2);
@@ -396,6 +403,7 @@ DM_FN void gamma_series_sums(double a, double x, double eps, double& B_out, doub
         }
         ap = a4; xn = x4; E = E4; B = B4;
     }
+#endif
     for (int n = n0; n <= 2000; ++n) {
         ap = ap + 1.0;
         xn = xn * x;
@@ -424,6 +432,7 @@ DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double&
     double P = b, Qd = 1.0;     // n (= 0)
     double di = 0.0;  // i as a double (exact), counted instead of converted each term
     int i0 = 1;
+#if DM_GPQ_BLOCKED
     for (; i0 + 1 <= 2000; i0 += 2) {
         const double d1 = di + 1.0, an1 = -d1 * (d1 - a), b1 = b + 2.0;
         const double P1 = DM_FMA(b1, P, an1 * Pm), Q1 = DM_FMA(b1, Qd, an1 * Qm);
@@ -437,6 +446,7 @@ DM_FN void gamma_cf_terms(double a, double x, double eps, double& P_out, double&
         if (t2) { P_out = P2; Qd_out = Q2; return; }
         di = d2; b = b2; Pm = P1; Qm = Q1; P = P2; Qd = Q2;
     }
+#endif
     for (int i = i0; i <= 2000; ++i) {
         di = di + 1.0;
         const double an = -di * (di - a);

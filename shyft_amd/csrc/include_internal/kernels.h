@@ -29,6 +29,7 @@ struct ptgsk_kargs {
     double* state_series;          // [PTGSK_NS][win_len+1][N] or null
     const uint8_t* active;         // [N] catchment filter or null
     int32_t* err;                  // [N]
+    double* hand;                  // [2][win_len][N] snow -> flux hand-over (gs sca, gs outflow), split launch
 };
 
 hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream);

@@ -132,6 +132,7 @@ struct shyft_hip_region {
 
     // device
     dbuf<double> d_params, d_cellc, d_state, d_forcing, d_resp, d_state_series;
+    dbuf<double> d_hand;  // pt_gs_k: [2][TW][n] gamma_snow -> flux hand-over of the split launch
     dbuf<int32_t> d_set_ix, d_err, d_doy, d_seg_cells, d_seg_off, d_sel;
     dbuf<int64_t> d_trel;
     dbuf<uint8_t> d_active;
@@ -1103,6 +1104,8 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
     a.active = h->active.empty() ? nullptr : h->d_active.p;
     a.err = h->d_err.p;
+    h->d_hand.alloc(2 * h->TW * h->n);
+    a.hand = h->d_hand.p;
     hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
     hip_check(launch_ptgsk_run(a, h->stream), "ptgsk_run_kernel launch");
     hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
