@@ -519,7 +519,12 @@ DM_FN double gamma_p(double a, double x) { return gamma_pq<dm_policy>(a, x, detm
 // digits10<d> to digits2 = (d+1)*1000/301 bits and stops its series / continued
 // fractions at a relative term size of ldexp(1, 1 - digits2):
 //   digits10<10> -> 36 bits -> 2^-35;  digits10<5> -> 19 bits -> 2^-18.
+// DETMATH_GAMMA_POLICY_FULL (oracle tolerance variants only): full double precision instead of the policy
+#ifdef DETMATH_GAMMA_POLICY_FULL
+DM_FN double gamma_snow_policy_eps(double) { return 2.220446049250313e-16; }
+#else
 DM_FN double gamma_snow_policy_eps(double a) { return a < 2.0 ? 0x1p-35 : 0x1p-18; }
+#endif
 
 }  // namespace detmath
 

@@ -27,10 +27,13 @@ _CACHE = {}
 
 
 def load(variant: str = "detmath"):
-    """variant 'detmath' (bit-exact checker of the HIP kernels) or 'libm' (host libm, as the reference)."""
+    """variant 'detmath' (bit-exact checker of the HIP kernels), 'libm' (host libm, as the reference),
+    'fullgamma' / 'libm_fullgamma' (gamma_snow's incomplete gamma at full precision: tolerance statement)."""
     if variant in _CACHE:
         return _CACHE[variant]
-    path = LIB if variant == "detmath" else os.path.join(ORACLE_DIR, "_build", "liboracle_libm.so")
+    names = {"detmath": None, "libm": "liboracle_libm.so", "fullgamma": "liboracle_fullgamma.so",
+             "libm_fullgamma": "liboracle_libm_fullgamma.so"}
+    path = LIB if variant == "detmath" else os.path.join(ORACLE_DIR, "_build", names[variant])
     if not os.path.exists(path):
         build()
     L = C.CDLL(path)
