@@ -345,7 +345,7 @@ class CatchmentSums:
 
 
 def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, btk_ms=None,
-             r_alt=None, sums=None):
+             r_alt=None, sums=None, walls=None, parts=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
     or IDW / BTK from the station network), then run_cells (and the routing group sums).
 
@@ -357,6 +357,7 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
         return _run_year_pipelined((r, r_alt), L, chunk, k_steps, seed, router, sums)
     kernel_ms = []
     for s in range(k_steps):
+        t_chunk = time.perf_counter()
         step0 = s * chunk
         # the chunk's forcing rows are all rewritten below and run_cells writes every response row of the
         # window, so the window moves without the NaN pre-fill of set_window
@@ -376,13 +377,23 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
                     r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
         r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
+        if parts is not None:
+            parts.append(r.last_run_kernel_ms())
         if sums is not None:
             sums.chunk(r, step0, chunk)
         if router is not None:
             router.chunk(r, step0, chunk)
+        if walls is not None:
+            _sync()
+            walls.append((time.perf_counter() - t_chunk) * 1e3)
     if router is not None:
         router.finish(k_steps * chunk)
     return kernel_ms
+
+
+def _sync():
+    import torch
+    torch.cuda.synchronize()
 
 
 def _run_year_pipelined(regs, L, chunk, k_steps, seed, router, sums):
@@ -547,12 +558,15 @@ def main():
     barrier_sync(pg, local)
     t0 = time.perf_counter()
     btk_ms = []
+    walls, parts = [], []
     kernel_ms = run_year(r, L, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
-                         r_alt=r_alt, sums=sums)
+                         r_alt=r_alt, sums=sums, walls=walls, parts=parts)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
     avg_kernel_ms = max_over_ranks(pg, local, float(np.mean(kernel_ms)))
+    # per-chunk wall (max over ranks) and the calendar year: the timed chunks 1-12 are Jan..Dec of one year
+    walls = [max_over_ranks(pg, local, w) for w in walls] if walls else []
 
     total_cell_steps = L.total * chunk * a.steps
     value = total_cell_steps / wall
@@ -596,6 +610,8 @@ def main():
         },
         "kernel_ms_per_step": avg_kernel_ms,
         "kernel_cell_steps_per_s": L.total * chunk / (avg_kernel_ms * 1e-3),
+        "chunk_wall_ms": [round(w, 2) for w in walls],
+        "chunk_kernel_ms": [round(k, 2) for k in kernel_ms],
         "roofline": {
             "bound": "hbm",
             "achieved": achieved / 1e9,
@@ -616,6 +632,18 @@ def main():
                     f"{state_b} B/cell state per launch (DESIGN.md)",
         },
     }
+    if len(walls) >= YEAR // chunk and chunk * (YEAR // chunk) == YEAR:
+        ny = YEAR // chunk
+        out["calendar_year"] = {
+            "value": L.total * chunk * ny / (sum(walls[:ny]) * 1e-3), "unit": "cell-steps/s",
+            "chunks": f"timed chunks 1-{ny} (Jan 1 - Dec 31, {YEAR} hourly steps: BASELINE configs[1]'s year)",
+            "ms_per_step": sum(walls[:ny]) / ny,
+            "kernel_ms_per_step": float(np.mean(kernel_ms[:ny])),
+            "note": "per-chunk wall clocks of this same timed run (synchronised at the end of each chunk)"}
+    if parts and len(parts[0]) == 2:
+        names = ("ptgsk_snow_kernel", "ptgsk_flux_kernel")
+        out["kernels"] = [{"name": names[k], "ms_per_step": float(np.mean([p[k] for p in parts])),
+                           "chunk_ms": [round(p[k], 2) for p in parts]} for k in range(2)]
     if a.btk:
         # the BTK time loop per chunk: one fp64 GEMM [cells x (S+3)] x [(S+3) x chunk], plus host
         # work (source rows, per-step beta); the full-set operators are built on the first chunk and reused

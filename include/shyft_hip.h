@@ -173,6 +173,10 @@ int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps);
 int shyft_hip_synchronize(shyft_hip_region* h);
 /* Milliseconds of the last run_cells kernel launch(es), timed with HIP events on the region's stream. */
 double shyft_hip_last_run_ms(const shyft_hip_region* h);
+/* The last run's kernels separately: pt_gs_k runs as two kernels (gamma_snow, then glacier/PT/AE/kirchner), the
+   other stacks as one. Fills ms[0..min(n, parts)) and returns the number of parts. (No reference counterpart:
+   measurement only.) */
+int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n);
 
 /* Response series for steps [step0, step0+n), [n][n_cells]. */
 int shyft_hip_get_series(const shyft_hip_region* h, int series, size_t step0, size_t n, double* dst, int dst_on_device);

@@ -1,0 +1,226 @@
+// gamma_snow's corr_lwc Brent job (gamma_snow.h:214-227), written for the one solver wavefront that runs it.
+//
+// In the pt_gs_k kernels a workgroup's Brent jobs are solved by one wavefront while the workgroup's other
+// wavefronts wait at a barrier (kernels/ptgsk.hip), so the job is a latency problem: a lone wavefront issues about
+// one instruction per 4-7 cycles whatever the instruction, so the solve costs its instruction count. This is the
+// same arithmetic as gs_corr_lwc (device/ptgsk_dev.h) -- the same Brent iterations (boost brent_find_minima), the
+// same f = (calc_q(a2, b2, z) - Q1)^2, the same incomplete-gamma terms and detmath exp / log fast paths -- with
+// fewer instructions around it:
+//  - no calls: exp, log, the series and the continued fraction are inline in the one loop;
+//  - the polynomial constants of exp and log are read once per job from a constant table into SGPRs and used as
+//    SGPR operands of v_fma_f64 (gs_fma_s), instead of two v_mov_b32 per constant per evaluation;
+//  - the series and continued fraction run without their 2^-200 rescale test: with shape a > 0 the series'
+//    E = (a+1)...(a+n) only grows, so a final E <= 2^200/... proves no term rescaled; the fraction's |P| is
+//    checked per term into a flag. A lane whose evaluation would have rescaled, or that leaves the fast domain
+//    (x <= 0, x not normal, a <= 0, |exp argument| > 708), is re-evaluated by the general gs_calc_q.
+// Bit-identical to gs_corr_lwc (tests: test_ptgsk_parity.py, tools/mb/mb_brent.cpp's device check).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ptgsk_dev.h"
+
+namespace shyft_dev {
+
+// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: 2/25 .. 2/3, LN2_HI LN2_LO
+static __constant__ double gsb_const[32] = {
+    1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
+    1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
+    2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04, 1.3888888888888889e-03,
+    8.3333333333333333e-03, 4.1666666666666664e-02, 1.6666666666666666e-01,
+    2.0 / 25, 2.0 / 23, 2.0 / 21, 2.0 / 19, 2.0 / 17, 2.0 / 15, 2.0 / 13, 2.0 / 11, 2.0 / 9, 2.0 / 7, 2.0 / 5,
+    2.0 / 3, 0.0, 0.0, 0.0, 0.0, 0.0};
+
+typedef __attribute__((address_space(4))) const double gsb_cdouble;
+
+// a * b + c with c an SGPR pair (wave-uniform constant): one v_fma_f64, no v_mov of the constant
+__device__ __forceinline__ double gs_fma_s(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+
+struct gsb_k {
+    double c[27];
+};
+
+__device__ __forceinline__ gsb_k gsb_load() {
+    const gsb_cdouble* __restrict__ p = (const gsb_cdouble*)gsb_const;
+    asm volatile("" : "+s"(p));  // keep the table opaque: scalar loads into SGPRs, not folded literals
+    gsb_k k;
+#pragma unroll
+    for (int i = 0; i < 27; ++i) k.c[i] = p[i];
+    return k;
+}
+
+// detmath::exp for |x| <= 708 (exp_poly + one ldexp)
+__device__ __forceinline__ double gsb_exp(double x, const gsb_k& k) {
+    const double t = x * k.c[0] + k.c[1];
+    const double kf = t - k.c[1];
+    double r = __builtin_fma(-kf, k.c[2], x);
+    r = __builtin_fma(-kf, k.c[3], r);
+    double p = gs_fma_s(r, k.c[4], k.c[5]);
+#pragma unroll
+    for (int i = 6; i <= 14; ++i) p = gs_fma_s(p, r, k.c[i]);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)kf);
+}
+
+// detmath::log for positive normal finite x (log_dd without its subnormal branch, hi part)
+__device__ __forceinline__ double gsb_log(double x, const gsb_k& k) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    int e = (int)((u >> 52) & 0x7ff) - 1023;
+    double m = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        e += 1;
+    }
+    const double f = m - 1.0;
+    const double d = 2.0 + f;
+    const double d_lo = (2.0 - d) + f;
+    const double s = f / d;
+    const double s_lo = (__builtin_fma(-s, d, f) - s * d_lo) / d;
+    const double z = s * s;
+    double t = gs_fma_s(k.c[15], z, k.c[16]);
+#pragma unroll
+    for (int i = 17; i <= 26; ++i) t = gs_fma_s(t, z, k.c[i]);
+    const double tail = (s * z) * t;
+    const double ed = (double)e;
+    const double a_hi = ed * k.c[2];
+    const double a_lo = ed * k.c[3];
+    const double b = 2.0 * s;
+    const double sum = a_hi + b;
+    const double bb = sum - a_hi;
+    const double err = (a_hi - (sum - bb)) + (b - bb);
+    const double small = ((err + 2.0 * s_lo) + tail) + a_lo;
+    return sum + small;
+}
+
+// calc_q(a, b, z) = a b P(a+1, z/b) + z (1 - P(a, z/b)) for the fast domain; ok = false: take gs_calc_q
+__device__ __forceinline__ double gsb_calc_q(double a, double b, double z, double lga, double eps, double ap1,
+                                             const gsb_k& k, bool& ok) {
+    const double x = z / b;
+    const double lx = gsb_log(x, k);
+    const double arg = a * lx - x - lga;
+    ok = x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308 && __builtin_fabs(arg) <= 708.0;
+    const double prefix = gsb_exp(arg, k);
+    double p, p1;
+    if (x < ap1) {
+        // series (detmath::gamma_series_sums without the rescale test: see the header)
+        double ap = a, E = 1.0, B = 0.0, xn = 1.0;
+        for (int n = 1; n <= 2000; ++n) {
+            ap = ap + 1.0;
+            xn = xn * x;
+            E = E * ap;
+            B = __builtin_fma(B, ap, xn);
+            if (xn < eps * (B + E)) break;
+        }
+        ok = ok && E <= detmath::GPQ_SCALE_HI;
+        const double aE = a * E;
+        const double pp = prefix * ((B + E) / aE);
+        const double pp1 = prefix * (B / aE);
+        p = pp < 1.0 ? pp : 1.0;
+        p1 = pp1 < 1.0 ? pp1 : 1.0;
+    } else {
+        // continued fraction (detmath::gamma_cf_terms, the rescale test folded into a flag)
+        double bcf = x + 1.0 - a;
+        double Pm = 1.0, Qm = 0.0, P = bcf, Qd = 1.0, di = 0.0;
+        bool big = false;
+        for (int i = 1; i <= 2000; ++i) {
+            di = di + 1.0;
+            const double an = -di * (di - a);
+            bcf = bcf + 2.0;
+            const double Pn = __builtin_fma(bcf, P, an * Pm);
+            const double Qn = __builtin_fma(bcf, Qd, an * Qm);
+            const double cross = Pn * Qd;
+            const double diff = cross - P * Qn;
+            Pm = P; Qm = Qd;
+            P = Pn; Qd = Qn;
+            if (__builtin_fabs(diff) <= eps * __builtin_fabs(cross)) break;
+            big = big || __builtin_fabs(P) > detmath::GPQ_SCALE_HI;
+        }
+        ok = ok && !big;
+        const double q = prefix * (Qd / P);
+        const double q1 = q + prefix / a;
+        const double pp = 1.0 - q;
+        const double pp1 = 1.0 - q1;
+        p = pp > 0.0 ? pp : 0.0;
+        p1 = pp1 > 0.0 ? pp1 : 0.0;
+    }
+    return a * b * p1 + z * (1.0 - p);
+}
+
+// the general evaluation, out of line (rare: Q1 without the opening state's gamma pair, or a lane outside the
+// fast domain)
+__device__ __noinline__ double gs_calc_q_general(double a, double b, double z, double lga) {
+    return gs_calc_q(a, b, z, lga);
+}
+
+__device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1, double a2, double b2, double q1,
+                                                double lga2) {
+    const double Q1 = q1 == q1 ? q1 : gs_calc_q_general(a1, b1, z1, dlgamma(a1));
+    const gsb_k k = gsb_load();
+    const double eps = detmath::gamma_snow_policy_eps(a2);
+    const double ap1 = a2 + 1.0;
+    const bool a_ok = a2 > 0.0;
+    auto f = [&](double z) {
+        bool ok;
+        double cq = gsb_calc_q(a2, b2, z, lga2, eps, ap1, k, ok);
+        if (!(ok && a_ok)) cq = gs_calc_q_general(a2, b2, z, lga2);  // the general path (rare)
+        const double v = cq - Q1;
+        return v * v;
+    };
+    double min = 0.0, max = z1;
+    const double tolerance = 0x1p-11;  // ldexp(1, 1-12)
+    const double golden = (double)0.3819660f;
+    double x, w, v, u, delta, delta2, fu, fv, fw, fx, mid, fract1, fract2;
+    x = w = v = max;
+    fw = fv = fx = f(x);
+    delta2 = delta = 0;
+    int count = 60;
+    do {
+        mid = (min + max) / 2;
+        fract1 = tolerance * fabs(x) + tolerance / 4;
+        fract2 = 2 * fract1;
+        if (fabs(x - mid) <= (fract2 - (max - min) / 2)) break;
+        if (fabs(delta2) > fract1) {
+            double r = (x - w) * (fx - fv);
+            double q = (x - v) * (fx - fw);
+            double p = (x - v) * q - (x - w) * r;
+            q = 2 * (q - r);
+            if (q > 0) p = -p;
+            q = fabs(q);
+            double td = delta2;
+            delta2 = delta;
+            if ((fabs(p) >= fabs(q * td / 2)) || (p <= q * (min - x)) || (p >= q * (max - x))) {
+                delta2 = (x >= mid) ? min - x : max - x;
+                delta = golden * delta2;
+            } else {
+                delta = p / q;
+                u = x + delta;
+                if (((u - min) < fract2) || ((max - u) < fract2)) delta = (mid - x) < 0 ? -fabs(fract1) : fabs(fract1);
+            }
+        } else {
+            delta2 = (x >= mid) ? min - x : max - x;
+            delta = golden * delta2;
+        }
+        u = (fabs(delta) >= fract1) ? (x + delta) : (delta > 0 ? x + fabs(fract1) : x - fabs(fract1));
+        fu = f(u);
+        if (fu <= fx) {
+            if (u >= x) min = x; else max = x;
+            v = w; w = x; x = u;
+            fv = fw; fw = fx; fx = fu;
+        } else {
+            if (u < x) min = u; else max = u;
+            if ((fu <= fw) || (w == x)) {
+                v = w; w = u; fv = fw; fw = fu;
+            } else if ((fu <= fv) || (v == x) || (v == w)) {
+                v = u; fv = fu;
+            }
+        }
+    } while (--count);
+    return x;
+}
+
+}  // namespace shyft_dev

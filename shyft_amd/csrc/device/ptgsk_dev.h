@@ -93,6 +93,10 @@ __device__ __forceinline__ double gs_calc_q_inl(double a, double b, double z, do
 #ifndef SHYFT_BRENT_INL
 #define SHYFT_BRENT_INL 0
 #endif
+// SHYFT_BRENT_ATTR: the Brent job as an out-of-line call (default) or inlined into the step loop
+#ifndef SHYFT_BRENT_ATTR
+#define SHYFT_BRENT_ATTR __noinline__
+#endif
 
 // corr_lwc (gamma_snow.h:214-227): boost brent_find_minima over [0, z1],
 // 12 bits, 60 iterations; golden constant is the float literal 0.3819660f.
@@ -105,7 +109,7 @@ __device__ __forceinline__ double gs_calc_q_inl(double a, double b, double z, do
 // else NaN
 // lga2 = lgamma(a2): the job's lane evaluates it (its lgamma cache needs it for the step's calc_snow_state after
 // the solve anyway), so the solving wavefront does not
-__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2,
+__device__ SHYFT_BRENT_ATTR double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2,
                                            double q1, double lga2 SHYFT_PROF_NF) {
 #ifdef SHYFT_ABLATE_BRENT
     return z1 * 0.5;  // timing ablation only (wrong results)

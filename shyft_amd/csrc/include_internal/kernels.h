@@ -32,7 +32,13 @@ struct ptgsk_kargs {
     double* hand;                  // [2][win_len][N] snow -> flux hand-over (gs sca, gs outflow), split launch
 };
 
-hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream);
+// SHYFT_PTGSK_SPLIT: run_cells of pt_gs_k as two kernels (gamma_snow, then the flux methods) with an HBM hand-over
+// instead of the fused step kernel. Measured slower, so off; kept for the record and for variants.
+#ifndef SHYFT_PTGSK_SPLIT
+#define SHYFT_PTGSK_SPLIT 0
+#endif
+// split launch (snow kernel, then flux kernel): ev_mid, if given, is recorded between the two
+hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t ev_mid = nullptr);
 
 struct hbv_kargs {
     int n_cells, step0, n_steps, win0, win_len, collect;

@@ -18,9 +18,21 @@
 #include <stdint.h>
 
 #include "../device/ptgsk_dev.h"
+#include "../device/gs_brent.h"
 #include "../include_internal/kernels.h"
 
 using namespace shyft_dev;
+
+// the Brent job of the solving wavefront: gs_corr_lwc_lean (device/gs_brent.h, the same arithmetic in fewer
+// instructions) or the reference-shaped gs_corr_lwc
+#ifndef SHYFT_BRENT_LEAN
+#define SHYFT_BRENT_LEAN 0
+#endif
+#if SHYFT_BRENT_LEAN
+#define GS_BRENT_JOB gs_corr_lwc_lean
+#else
+#define GS_BRENT_JOB gs_corr_lwc
+#endif
 
 #ifdef SHYFT_PROF
 // phase timing (profiling builds only): per-wavefront s_memtime deltas summed over the launch
@@ -253,7 +265,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const 
                 // barrier below): it gets issue priority over the other workgroups' wavefronts on its SIMD
                 if (t < nj) __builtin_amdgcn_s_setprio(SHYFT_BRENT_PRIO);
 #endif
-                for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
+                for (int j = t; j < nj; j += BLOCK) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
 #if SHYFT_BRENT_PRIO > 0
                 __builtin_amdgcn_s_setprio(0);
 #endif
@@ -450,7 +462,7 @@ __global__ __launch_bounds__(BLOCK, SHYFT_SNOW_WAVES) void ptgsk_snow_kernel(con
             int nf = 0;
             for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j], nf);
 #else
-            for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
+            for (int j = t; j < nj; j += BLOCK) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
 #endif
 #if SHYFT_BRENT_PRIO > 0
             __builtin_amdgcn_s_setprio(0);
@@ -513,7 +525,6 @@ __global__ __launch_bounds__(BLOCK, SHYFT_FLUX_WAVES) void ptgsk_flux_kernel(con
     const size_t RS = TW * N;
     const double* __restrict__ H = a.hand;
     double* __restrict__ SS = a.state_series;
-    const size_t SSS = (TW + 1) * N;
 
     const int i_end = a.step0 + a.n_steps;
     for (int i = a.step0; i < i_end; ++i) {
@@ -561,29 +572,29 @@ __global__ __launch_bounds__(BLOCK, SHYFT_FLUX_WAVES) void ptgsk_flux_kernel(con
 
 }  // namespace
 
-#ifndef SHYFT_PTGSK_SPLIT
-#define SHYFT_PTGSK_SPLIT 1
-#endif
 
 #ifndef SHYFT_COMPACT_DEFAULT
 #define SHYFT_COMPACT_DEFAULT 1
 #endif
 
-hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream) {
+hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t ev_mid) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
     if (SHYFT_PTGSK_SPLIT && a.hand) {
-        if (a.fcol) {
-            hipLaunchKernelGGL((ptgsk_snow_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            hipLaunchKernelGGL((ptgsk_flux_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        } else if (a.uniform_params) {
-            hipLaunchKernelGGL((ptgsk_snow_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            hipLaunchKernelGGL((ptgsk_flux_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        } else {
-            hipLaunchKernelGGL((ptgsk_snow_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            hipLaunchKernelGGL((ptgsk_flux_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        }
+        if (a.fcol) hipLaunchKernelGGL((ptgsk_snow_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else if (a.uniform_params) hipLaunchKernelGGL((ptgsk_snow_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else hipLaunchKernelGGL((ptgsk_snow_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (ev_mid && (e = hipEventRecord(ev_mid, stream)) != hipSuccess) return e;
+        if (a.fcol) hipLaunchKernelGGL((ptgsk_flux_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else if (a.uniform_params) hipLaunchKernelGGL((ptgsk_flux_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else hipLaunchKernelGGL((ptgsk_flux_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
         return hipGetLastError();
+    }
+    if (ev_mid) {
+        hipError_t e = hipEventRecord(ev_mid, stream);
+        if (e != hipSuccess) return e;
     }
     if (a.fcol)
         hipLaunchKernelGGL((ptgsk_run_kernel<true, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);

@@ -106,10 +106,12 @@ struct shyft_hip_region {
     size_t n = 0;
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;  // ev_mid: between the split pt_gs_k kernels
     hipEvent_t ev_copy = nullptr;  // shyft_hip_copy_state: the copy out of this region's state has finished
     std::string err;
     double last_ms = 0.0;
+    double last_part_ms[2] = {0.0, 0.0};  // pt_gs_k: snow kernel, flux kernel (split launch)
+    int last_parts = 1;
 
     // host mirrors
     std::vector<double> geo;  // n x 11
@@ -480,6 +482,7 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
         hip_check(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
         hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
         hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
+        hip_check(hipEventCreate(&h->ev_mid), "hipEventCreate");
         hip_check(hipEventCreateWithFlags(&h->ev_copy, hipEventDisableTiming), "hipEventCreate");
         h->d_state.alloc(h->n_state_fields() * n_cells);
         h->d_err.alloc(n_cells);
@@ -500,6 +503,7 @@ void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->ev_mid) (void)hipEventDestroy(h->ev_mid);
     if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1104,11 +1108,15 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
     a.active = h->active.empty() ? nullptr : h->d_active.p;
     a.err = h->d_err.p;
-    h->d_hand.alloc(2 * h->TW * h->n);
-    a.hand = h->d_hand.p;
+    a.hand = nullptr;
+    if (SHYFT_PTGSK_SPLIT) {
+        h->d_hand.alloc(2 * h->TW * h->n);
+        a.hand = h->d_hand.p;
+    }
     hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
-    hip_check(launch_ptgsk_run(a, h->stream), "ptgsk_run_kernel launch");
+    hip_check(launch_ptgsk_run(a, h->stream, SHYFT_PTGSK_SPLIT ? h->ev_mid : nullptr), "ptgsk_run_kernel launch");
     hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
+    h->last_parts = SHYFT_PTGSK_SPLIT ? 2 : 1;
 }
 
 static void finish_run(shyft_hip_region* h) {
@@ -1119,6 +1127,14 @@ static void finish_run(shyft_hip_region* h) {
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
     h->last_ms = ms;
+    h->last_part_ms[0] = ms;
+    h->last_part_ms[1] = 0.0;
+    if (h->last_parts == 2) {
+        float m0 = 0.f;
+        hip_check(hipEventElapsedTime(&m0, h->ev0, h->ev_mid), "hipEventElapsedTime");
+        h->last_part_ms[0] = m0;
+        h->last_part_ms[1] = ms - m0;
+    }
     // the per-cell error codes stay on the device: one reduction to the lowest failing cell, 8 bytes back
     const int32_t none = INT32_MAX;
     hip_check(hipMemcpyAsync(h->d_flag.p, &none, sizeof(int32_t), hipMemcpyHostToDevice, h->stream), "upload flag");
@@ -1184,6 +1200,12 @@ int shyft_hip_synchronize(shyft_hip_region* h) {
 }
 
 double shyft_hip_last_run_ms(const shyft_hip_region* h) { return h ? h->last_ms : 0.0; }
+
+int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n) {
+    if (!h) return 0;
+    for (int k = 0; k < n && k < h->last_parts; ++k) ms[k] = h->last_part_ms[k];
+    return h->last_parts;
+}
 
 int shyft_hip_get_series(const shyft_hip_region* hc, int series, size_t step0, size_t n, double* dst, int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);

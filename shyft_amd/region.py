@@ -173,6 +173,12 @@ class HipRegion:
     def last_run_ms(self) -> float:
         return float(self._L.shyft_hip_last_run_ms(self.h))
 
+    def last_run_kernel_ms(self) -> list:
+        """The last run's kernels separately (pt_gs_k: [snow kernel, flux kernel]; other stacks: [kernel])."""
+        buf = (C.c_double * 4)()
+        n = self._L.shyft_hip_last_run_kernel_ms(self.h, buf, 4)
+        return [float(buf[k]) for k in range(n)]
+
     def get_series(self, series: int, step0: int, n: int) -> np.ndarray:
         out = np.empty((n, self.n), dtype=np.float64)
         self._chk(self._L.shyft_hip_get_series(self.h, series, step0, n, _ptr(out), 0))

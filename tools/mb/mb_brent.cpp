@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <vector>
 #include "../../shyft_amd/csrc/device/ptgsk_dev.h"
+#include "../../shyft_amd/csrc/device/gs_brent.h"
 using namespace shyft_dev;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
@@ -15,6 +16,37 @@ __global__ void prep(const double* J, double* q1, double* lga2, int n) {
     const double* j = J + 5 * i;
     q1[i] = gs_calc_q(j[1], j[2], j[0], dlgamma(j[1]));
     lga2[i] = dlgamma(j[3]);
+}
+
+// the lean solver against gs_corr_lwc on every job, bit for bit (q1 given, and q1 = NaN)
+__global__ void check_lean(const double* J, const double* q1, const double* lga2, int n, int* bad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* j = J + 5 * i;
+    for (int mode = 0; mode < 2; ++mode) {
+        const double q = mode ? __builtin_nan("") : q1[i];
+        const double r0 = gs_corr_lwc(j[0], j[1], j[2], j[3], j[4], q, lga2[i]);
+        const double r1 = gs_corr_lwc_lean(j[0], j[1], j[2], j[3], j[4], q, lga2[i]);
+        if (__double_as_longlong(r0) != __double_as_longlong(r1)) atomicAdd(bad, 1);
+    }
+}
+
+template <int LEAN>
+__global__ __launch_bounds__(64) void solve2(const double* J, const double* q1, const double* lga2, int n, int reps,
+                                             int active, double* out, unsigned long long* cyc) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (int)(((unsigned long long)g * 7919ull) % (unsigned long long)n);
+    const double* j = J + 5 * i;
+    double z1 = j[0], a1 = j[1], b1 = j[2], a2 = j[3], b2 = j[4], q = q1[i], lg = lga2[i];
+    double acc = 0.0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if ((int)(threadIdx.x & 63) < active)
+        for (int r = 0; r < reps; ++r)
+            acc += LEAN ? gs_corr_lwc_lean(z1 + 0.0 * acc, a1, b1, a2, b2, q, lg)
+                        : gs_corr_lwc(z1 + 0.0 * acc, a1, b1, a2, b2, q, lg);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[g] = acc;
+    if ((threadIdx.x & 63) == 0) cyc[g / 64] = t1 - t0;
 }
 
 // every lane solves job (gid % n), reps times (each solve's z1 depends on the previous result by +0*r)
@@ -88,6 +120,28 @@ int main(int argc, char** argv) {
     prep<<<(n + 63) / 64, 64>>>(J, q1, lg, n);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    {
+        int* bad; int hb = 0;
+        CK(hipMalloc(&bad, 4)); CK(hipMemcpy(bad, &hb, 4, hipMemcpyHostToDevice));
+        check_lean<<<(n + 63) / 64, 64>>>(J, q1, lg, n, bad);
+        CK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
+        printf("lean vs gs_corr_lwc: %d of %d results differ\n", hb, 2 * n);
+    }
+    for (int lean = 0; lean < 2; ++lean) for (int active : {64, 22}) for (int waves : {1, 1024, 4096}) {
+        const int reps = 4;
+        auto go = [&]() {
+            if (lean) solve2<1><<<waves, 64>>>(J, q1, lg, n, reps, active, out, cyc);
+            else solve2<0><<<waves, 64>>>(J, q1, lg, n, reps, active, out, cyc);
+        };
+        go();
+        CK(hipEventRecord(e0)); go(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        std::vector<unsigned long long> c(waves);
+        CK(hipMemcpy(c.data(), cyc, waves * 8, hipMemcpyDeviceToHost));
+        printf("%s active %2d waves %5d: %8.0f cyc/job (per wave), %.3g jobs/s\n", lean ? "lean " : "brent", active,
+               waves, mean_cyc(c) / reps, (double)waves * active * reps / (ms * 1e-3));
+    }
+    if (getenv("MB_LEAN")) { printf("MB_DONE\n"); return 0; }
     // Brent jobs: waves = 1, 256 (1/CU), 1024 (1/SIMD), 4096 (4/SIMD), 8192
     const int reps = 4;
     for (int active : {64, 22}) for (int waves : {1, 1024, 4096}) {
