@@ -457,7 +457,7 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
 
 
 def workload_tag(a, cells):

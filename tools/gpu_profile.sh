@@ -10,7 +10,7 @@
 set -o pipefail
 R=$(pwd)
 ARGS=${BENCH_ARGS:---gpus 1 --steps 20 --warmup 5}
-ROUND=${ROUND:-r02}
+ROUND=${ROUND:-r03}
 KERNEL=${KERNEL:-ptgsk_run_kernel}
 cd /tmp && export TMPDIR=/tmp
 run() {  # name, rocprofv3 args...
