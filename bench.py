@@ -72,6 +72,9 @@ def parse(argv=None):
                     help="skip the per-chunk catchment discharge sums (cell_statistics, RCCL allgather)")
     ap.add_argument("--dump-sums", default="",
                     help="rank 0 saves the region's catchment discharge sums [C][T] (.npy) after the timed steps")
+    ap.add_argument("--dump-route", default="",
+                    help="rank 0 saves the routed river series (local, upstream, output) [3][R][T] (.npy) after the "
+                         "timed steps")
     ap.add_argument("--dist-check", action="store_true",
                     help="launcher/rendezvous/collective rehearsal without the GPU: every rank combines "
                          "catchment sums of a synthetic series over its shard, rank 0 checks them against "
@@ -683,6 +686,8 @@ def main():
                                       f"device after the last chunk)")
         out["routing"] = {"rivers": len(router.rivers), "groups": router.G,
                           "outlet_mean_m3s": float(o[0].mean()), "outlet_max_m3s": float(o[0].max())}
+        if a.dump_route and rank == 0:
+            np.save(a.dump_route, np.stack(router.out))
     if sums is not None:
         T = a.steps * chunk
         tot = sums.sums[:, :T]

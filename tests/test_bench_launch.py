@@ -61,3 +61,28 @@ def test_two_ranks_one_gpu_catchment_sums_match_single_rank(stack, tmp_path):
     s1, s2 = np.load(tmp_path / "s1.npy"), np.load(tmp_path / "s2.npy")
     assert s1.shape == (100, 144) and np.isfinite(s1).all() and s1.sum() > 0
     assert np.array_equal(s1, s2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,cells", [(2, 4096), (3, 4099)])
+def test_sharded_routing_matches_single_rank(world, cells, tmp_path):
+    """configs[4]'s routing (core/routing.h:344-383) through the real multi-rank bench path: every rank forms the
+    (river, UHG) group sums of its own cells, the partials are all-gathered and added in rank order, then every rank
+    convolves the river network. Two ranks split 4096 cells on a catchment boundary, so each group is summed on
+    one rank and the result must equal one rank's bit for bit; three ranks over 4099 cells split groups between
+    ranks, so the group sums reassociate: the routed series then agree within 1e-12 of their magnitude."""
+    common = ["--stack", "pt_ss_k", "--total-cells", str(cells), "--catchments", "100", "--chunk", "48", "--steps",
+              "3", "--warmup", "0", "--no-cpu-baseline", "--no-catchment-sums"]
+    p1, o1 = _bench(["--gpus", "1", "--dump-route", str(tmp_path / "r1.npy")] + common)
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    pn, on = _bench(["--gpus", str(world), "--dump-route", str(tmp_path / "rn.npy")] + common,
+                    env_extra={"SHYFT_DIST_BACKEND": "gloo"})
+    assert pn.returncode == 0, pn.stderr[-2000:]
+    assert o1["n_gpus"] == 1 and on["n_gpus"] == world and "routing" in on
+    r1, rn = np.load(tmp_path / "r1.npy"), np.load(tmp_path / "rn.npy")
+    assert r1.shape[0] == 3 and r1.shape[2] == 144 and np.isfinite(r1).all() and r1[2].sum() > 0
+    if world == 2:
+        assert np.array_equal(r1, rn)
+    else:
+        scale = np.abs(r1).max()
+        assert np.max(np.abs(r1 - rn)) <= 1e-12 * scale
