@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fastmath.h"
 #include "pt_dev.h"
 #include "special.h"
 #include "../include_internal/layout.h"
@@ -431,10 +432,25 @@ __device__ inline double gs_solve_lwc(const gs_mid& m) {
 }
 
 // ------------------------------------------------------------------ kirchner
+// SHYFT_K_FM: kirchner's exps inline with their constants in SGPRs (device/fastmath.h), loaded once per step
+#ifndef SHYFT_K_FM
+#define SHYFT_K_FM 0
+#endif
+#if SHYFT_K_FM
+#define K_EXP(x) fm_exp((x), ek)
+#define K_EXP_DECL const fm_exp_k ek = fm_exp_load();
+#define K_EXP_ARG , const fm_exp_k& ek
+#define K_EXP_PASS , ek
+#else
+#define K_EXP(x) dexp(x)
+#define K_EXP_DECL
+#define K_EXP_ARG
+#define K_EXP_PASS
+#endif
 // kirchner.h:186-198
-__device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, double c2, double c3) {
-    const double g = dexp(c1 + c2 * ln_q + c3 * ln_q * ln_q);
-    return g >= 1.e-30 ? g * (p_minus_e * dexp(-ln_q) - 1.0) : 0.0;
+__device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, double c2, double c3 K_EXP_ARG) {
+    const double g = K_EXP(c1 + c2 * ln_q + c3 * ln_q * ln_q);
+    return g >= 1.e-30 ? g * (p_minus_e * K_EXP(-ln_q) - 1.0) : 0.0;
 }
 
 // kirchner::calculator::step with trapezoidal_average (kirchner.h:23-53, 213-235).
@@ -445,13 +461,14 @@ __device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, do
 __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, double e, double t1, double c1, double c2,
                                      double c3) {
     const double abs_err = 1.0e-7, rel_err = 1.0e-8;
+    K_EXP_DECL
     if (q < 0.00001) q = 0.00001;
 #ifdef SHYFT_ABLATE_KIRCHNER
     q_avg = q; q = q + 0.01 * (p - e); return true;  // timing ablation only (wrong results)
 #endif
     const double pe = p - e;
     double x = dlog(q);
-    double dxdt = kirchner_f(x, pe, c1, c2, c3);
+    double dxdt = kirchner_f(x, pe, c1, c2, c3 K_EXP_PASS);
     double t = 0.0, dt = t1;
     double x_old = x, dxdt_old = dxdt, t_old = 0.0;
     double k3 = 0, k4 = 0, k5 = 0, k6 = 0;
@@ -469,21 +486,21 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
                  dc5 = c5_ - -92097.0 / 339200, dc6 = c6_ - 187.0 / 2100, dc7 = -1.0 / 40;
     while (t < t1) {
         double xt = 1.0 * x + dt * b21 * dxdt;
-        const double k2 = kirchner_f(xt, pe, c1, c2, c3);
+        const double k2 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
         xt = 1.0 * x + dt * b31 * dxdt + dt * b32 * k2;
-        const double s3 = kirchner_f(xt, pe, c1, c2, c3);
+        const double s3 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
         xt = 1.0 * x + dt * b41 * dxdt + dt * b42 * k2 + dt * b43 * s3;
-        const double s4 = kirchner_f(xt, pe, c1, c2, c3);
+        const double s4 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
         xt = 1.0 * x + dt * b51 * dxdt + dt * b52 * k2 + dt * b53 * s3 + dt * b54 * s4;
-        const double s5 = kirchner_f(xt, pe, c1, c2, c3);
+        const double s5 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
         xt = 1.0 * x + dt * b61 * dxdt + dt * b62 * k2 + dt * b63 * s3 + dt * b64 * s4 + dt * b65 * s5;
-        const double s6 = kirchner_f(xt, pe, c1, c2, c3);
+        const double s6 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
         const double xo = 1.0 * x + dt * c1_ * dxdt + dt * c3_ * s3 + dt * c4_ * s4 + dt * c5_ * s5 + dt * c6_ * s6;
-        const double dxdt_o = kirchner_f(xo, pe, c1, c2, c3);
+        const double dxdt_o = kirchner_f(xo, pe, c1, c2, c3 K_EXP_PASS);
         const double xerr = dt * dc1 * dxdt + dt * dc3 * s3 + dt * dc4 * s4 + dt * dc5 * s5 + dt * dc6 * s6 + dt * dc7 * dxdt_o;
         const double err = fabs(xerr) / (abs_err + rel_err * (1.0 * fabs(x) + 1.0 * dt * fabs(dxdt)));
         if (err > 1.0) {
-            dt = dt * smax(0.9 * dpowr(err, -1.0 / 3.0), 1.0 / 5.0);
+            dt = dt * smax(0.9 * K_EXP(-1.0 / 3.0 * dlog(err)), 1.0 / 5.0);  // dpowr(err, -1/3)
             if (++attempts >= 500) { ok = false; break; }
             continue;
         }
@@ -492,13 +509,13 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         t = t + dt;
         if (err < 0.5) {
             const double e2 = smax(0.00032, err);  // dpow(5.0, -5.0)
-            dt = dt * (9.0 / 10.0 * dpowr(e2, -1.0 / 5.0));
+            dt = dt * (9.0 / 10.0 * K_EXP(-1.0 / 5.0 * dlog(e2)));  // dpowr(e2, -1/5)
         }
         x_old = x; dxdt_old = dxdt;
         x = xo; dxdt = dxdt_o;
         k3 = s3; k4 = s4; k5 = s5; k6 = s6;
         if (t < t1) {
-            const double fv = dexp(x);
+            const double fv = K_EXP(x);
             area += 0.5 * (f_a + fv) * (t - t_a);
             f_a = fv;
             t_a = t;
@@ -530,7 +547,7 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         x = 1.0 * x_old + h * b1_theta * dxdt_old + h * b3_theta * k3 + h * b4_theta * k4 + h * b5_theta * k5 +
             h * b6_theta * k6 + h * b7_theta * dxdt;
     }
-    q = dexp(x);
+    q = K_EXP(x);
     area += 0.5 * (f_a + q) * (t1 - t_a);
     q_avg = area / (t1 - 0.0);
     return ok;

@@ -16,6 +16,7 @@
 // per-lane version: the same function on the same arguments.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../device/ptgsk_dev.h"
 #include "../device/gs_brent.h"
@@ -77,8 +78,11 @@ constexpr int BLOCK = SHYFT_BLOCK;
 #ifndef SHYFT_PTGSK_LDSC
 #define SHYFT_PTGSK_LDSC 1
 #endif
-template <bool COMPACT, bool UNIFORM, bool ENS = false>
-__global__ __launch_bounds__(BLOCK, SHYFT_LB_WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
+// WAVES: the occupancy target. 4 waves per SIMD (128 VGPRs, spilling) is the measured best when the launch fills
+// the GPU; a region too small to give every SIMD 4 waves (<= 2 workgroups per CU, e.g. a strong-scaled shard of
+// 131K cells) gets the 2-wave instance instead (256 VGPRs, no spills): it cannot be 4-deep anyway.
+template <bool COMPACT, bool UNIFORM, bool ENS = false, int WAVES = SHYFT_LB_WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
     if (valid && a.active && !a.active[cell]) valid = false;
@@ -596,11 +600,27 @@ hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t
         hipError_t e = hipEventRecord(ev_mid, stream);
         if (e != hipSuccess) return e;
     }
+    // workgroups resident at 4 waves per SIMD: 4 per CU (16 waves of 256-lane workgroups)
+    int n_cu = 256;
+    {
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            int v = 0;
+            if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) n_cu = v;
+        }
+    }
+    static const char* force = getenv("SHYFT_PTGSK_WAVES");  // measurement knob: "2" / "4" forces an instance
+    const bool small = force ? force[0] == '2' : grid <= 2 * n_cu;
     if (a.fcol)
         hipLaunchKernelGGL((ptgsk_run_kernel<true, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (SHYFT_COMPACT_DEFAULT)
-        if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        if (a.uniform_params) {
+            if (small) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
+            else hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        } else {
+            if (small) hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
+            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        }
     else
         hipLaunchKernelGGL((ptgsk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
