@@ -88,6 +88,9 @@ def parse(argv=None):
     ap.add_argument("--pipeline", action="store_true",
                     help="two regions: generate chunk s+1's forcing while chunk s runs (measured slower for pt_gs_k, "
                          "see DESIGN.md section 5; off by default)")
+    ap.add_argument("--overlap-forcing", type=int, default=0, metavar="CUS",
+                    help="generate chunk s+1's forcing into a second window buffer on a side stream of CUS CUs while "
+                         "chunk s runs (0: generate each chunk before its run)")
     ap.add_argument("--chunk", type=int, default=CHUNK)
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
@@ -348,7 +351,7 @@ class CatchmentSums:
 
 
 def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, btk_ms=None,
-             r_alt=None, sums=None, walls=None, parts=None):
+             r_alt=None, sums=None, walls=None, parts=None, overlap=0):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
     or IDW / BTK from the station network), then run_cells (and the routing group sums).
 
@@ -358,6 +361,8 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
     Every chunk's forcing is still produced inside the timed region; the generator just no longer adds to it."""
     if r_alt is not None and stations is None:
         return _run_year_pipelined((r, r_alt), L, chunk, k_steps, seed, router, sums)
+    if overlap and stations is None:
+        return _run_year_overlapped(r, L, chunk, k_steps, seed, router, sums, walls, parts, overlap)
     kernel_ms = []
     for s in range(k_steps):
         t_chunk = time.perf_counter()
@@ -397,6 +402,37 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
 def _sync():
     import torch
     torch.cuda.synchronize()
+
+
+def _run_year_overlapped(r, L, chunk, k_steps, seed, router, sums, walls, parts, n_cus):
+    """As run_year with the device generator, but chunk s+1's forcing is generated into the region's second window
+    buffer on a side stream of n_cus CUs while chunk s runs (shyft_hip_prefetch_synthetic_forcing), and the buffers
+    swap before chunk s+1 (the run waits for the generator on the device). Chunk 0's forcing is generated before
+    its run, inside the timed region like every other chunk's."""
+    kernel_ms = []
+    r.move_window(0, 0)
+    r.synthetic_forcing(seed, 0, chunk, cell_offset=L.off)
+    for s in range(k_steps):
+        t_chunk = time.perf_counter()
+        step0 = s * chunk
+        if s + 1 < k_steps:
+            r.prefetch_synthetic_forcing(seed, step0 + chunk, cell_offset=L.off, n_cus=n_cus)
+        r.run_cells(0, step0, chunk)
+        kernel_ms.append(r.last_run_ms())
+        if parts is not None:
+            parts.append(r.last_run_kernel_ms())
+        if sums is not None:
+            sums.chunk(r, step0, chunk)
+        if router is not None:
+            router.chunk(r, step0, chunk)
+        if s + 1 < k_steps:
+            r.swap_forcing_window(step0 + chunk)
+        if walls is not None:
+            _sync()
+            walls.append((time.perf_counter() - t_chunk) * 1e3)
+    if router is not None:
+        router.finish(k_steps * chunk)
+    return kernel_ms
 
 
 def _run_year_pipelined(regs, L, chunk, k_steps, seed, router, sums):
@@ -556,14 +592,15 @@ def main():
     # warmup (untimed): W chunks from Jan 1, then state is reset for the timed year
     if a.warmup > 0:
         r.set_state(state0)
-        run_year(r, L, chunk, a.warmup, synthetic.SEED, stations, router, a.btk, r_alt=r_alt, sums=sums)
+        run_year(r, L, chunk, a.warmup, synthetic.SEED, stations, router, a.btk, r_alt=r_alt, sums=sums,
+                 overlap=a.overlap_forcing)
     r.set_state(state0)   # the initial state is an input: resident in HBM before the timed region
     barrier_sync(pg, local)
     t0 = time.perf_counter()
     btk_ms = []
     walls, parts = [], []
     kernel_ms = run_year(r, L, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
-                         r_alt=r_alt, sums=sums, walls=walls, parts=parts)
+                         r_alt=r_alt, sums=sums, walls=walls, parts=parts, overlap=a.overlap_forcing)
     barrier_sync(pg, local)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
@@ -604,6 +641,8 @@ def main():
             "catchments": L.n_catch,
             "steps_per_chunk": chunk,
             "forcing": ("IDW/BTK from stations, per chunk, before its run" if a.idw else
+                        f"device generator, chunk s+1 into a second window buffer on a {a.overlap_forcing}-CU side "
+                        "stream while chunk s runs (chunk 1 before its run)" if a.overlap_forcing else
                         "device generator, per chunk, overlapped with the previous chunk's run (two regions, state "
                         "handed over device to device)" if r_alt is not None else
                         "device generator, per chunk, before its run"),

@@ -171,6 +171,13 @@ int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, i
 /* Asynchronous variant on the region's stream (no argument re-validation of state). */
 int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps);
 int shyft_hip_synchronize(shyft_hip_region* h);
+/* Double-buffered forcing window (measurement / pipelining aid, no reference counterpart): generate the synthetic
+   forcing of the window starting at w0_next into a second buffer on a side stream restricted to n_cus CUs (<= 0:
+   no restriction) while the current window runs; shyft_hip_swap_forcing_window(h, w0_next) then makes it the
+   region's window (the next run waits for the generator on the device). */
+int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t w0_next,
+                                         int n_cus);
+int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next);
 /* Milliseconds of the last run_cells kernel launch(es), timed with HIP events on the region's stream. */
 double shyft_hip_last_run_ms(const shyft_hip_region* h);
 /* The last run's kernels separately: pt_gs_k runs as two kernels (gamma_snow, then glacier/PT/AE/kirchner), the

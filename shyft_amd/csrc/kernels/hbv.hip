@@ -49,6 +49,12 @@ constexpr int BLOCK = 256;
 #ifndef SHYFT_HBV_NT
 #define SHYFT_HBV_NT 0
 #endif
+#ifndef SHYFT_HBV_POW2
+#define SHYFT_HBV_POW2 1
+#endif
+#ifndef SHYFT_HBV_PRELOAD
+#define SHYFT_HBV_PRELOAD 0
+#endif
 #if SHYFT_HBV_NT
 #define HBV_LD(p) __builtin_nontemporal_load(&(p))
 #define HBV_ST(p, v) __builtin_nontemporal_store((v), &(p))
@@ -67,7 +73,38 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     const size_t NF = a.fcol ? (size_t)a.f_cols : N;
     const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
     const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * HBV_NP;
-
+#if SHYFT_HBV_PRELOAD
+    // the uniform parameter row is read again in every step (scalar loads, constant-cache hits) instead of held
+    // in SGPRs across the time loop: the row (22 values + 2 x NB bin values) does not fit next to the loop's own
+    // SGPRs, and the compiler's SGPR spills to VGPR lanes cost a v_readlane_b32 (VALU issue) per use
+#define HBV_PARAMS()                                                                        \
+    const double* __restrict__ Pq = P;                                                      \
+    if (UNIFORM) asm volatile("" : "+s"(Pq));                                               \
+    hbv_snow_par_t<NB> sp_par;                                                              \
+    sp_par.nb = (int)Pq[HK_NB];                                                             \
+    _Pragma("unroll") for (int i_ = 0; i_ < NB; ++i_) {                                     \
+        sp_par.s[i_] = Pq[HK_S0 + i_];                                                      \
+        sp_par.I[i_] = Pq[HK_I0 + i_];                                                      \
+    }                                                                                       \
+    sp_par.tx = Pq[HK_TX]; sp_par.cx = Pq[HK_CX]; sp_par.ts = Pq[HK_TS]; sp_par.lw = Pq[HK_LW]; \
+    sp_par.cfr = Pq[HK_CFR];                                                                \
+    const double fc = Pq[HK_FC], beta = Pq[HK_BETA], lp = Pq[HK_LP];                        \
+    const double uz1 = Pq[HK_UZ1], kuz2 = Pq[HK_KUZ2], kuz1 = Pq[HK_KUZ1], perc = Pq[HK_PERC], klz = Pq[HK_KLZ]; \
+    const double p_corr = Pq[HK_PCORR], pt_albedo = Pq[HK_PT_ALBEDO], pt_alpha = Pq[HK_PT_ALPHA], dtf = Pq[HK_DTF]; \
+    const double gm_direct = Pq[HK_GM_DIRECT];                                              \
+    const double gm_routed = 1 - gm_direct;
+    hbv_snow_par_t<NB> sp_par0;
+    sp_par0.nb = (int)P[HK_NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        sp_par0.s[i] = P[HK_S0 + i];
+        sp_par0.I[i] = P[HK_I0 + i];
+    }
+    sp_par0.tx = P[HK_TX]; sp_par0.cx = P[HK_CX]; sp_par0.ts = P[HK_TS]; sp_par0.lw = P[HK_LW]; sp_par0.cfr = P[HK_CFR];
+#define sp_par_init sp_par0
+#else
+#define HBV_PARAMS()
+#define sp_par_init sp_par
     hbv_snow_par_t<NB> sp_par;
     sp_par.nb = (int)P[HK_NB];
 #pragma unroll
@@ -85,6 +122,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     const double p_corr = P[HK_PCORR], pt_albedo = P[HK_PT_ALBEDO], pt_alpha = P[HK_PT_ALPHA], dtf = P[HK_DTF];
     const double gm_direct = P[HK_GM_DIRECT];
     const double gm_routed = 1 - gm_direct;
+#endif
 
     const double* __restrict__ cc = a.cellc;
     const double glacier_fraction = cc[HC_GLACIER * N + cell];
@@ -108,9 +146,9 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         sw[i] = i < nbs ? st[(HS_SW0 + i) * N + cell] : 0.0;
     }
     // state.snow.distribute(parameter.snow, false) (hbv_stack.h:310): only on a bin-count mismatch
-    if ((int)nb_state != sp_par.nb) {
-        hbv_distribute(sp_par, sp, sw, swe, sca);
-        nb_state = (double)sp_par.nb;
+    if ((int)nb_state != sp_par_init.nb) {
+        hbv_distribute(sp_par_init, sp, sw, swe, sca);
+        nb_state = (double)sp_par_init.nb;
     }
     int32_t err = 0;
 
@@ -153,6 +191,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         }
     }
     for (int i = a.step0; i < i_end; ++i) {
+        HBV_PARAMS()
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
         const double temp = rt[0], rad = rr[0], rel_hum = rh[0], prec_raw = rp[0];
@@ -180,7 +219,14 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         // hbv_soil::step (hbv_soil.h:55-64)
         const double soil_temp = sm + snow_outflow;
+#if SHYFT_HBV_POW2
+        // detmath::pow returns x * x for y == 2 (the default beta): beta is wave-uniform with one parameter set, so
+        // this takes a scalar branch instead of a call (whose entry would wait for the prefetched forcing)
+        const double soil_x = soil_temp / fc;
+        const double soil_q = snow_outflow * (beta == 2.0 ? soil_x * soil_x : dpow(soil_x, beta));
+#else
         const double soil_q = snow_outflow * dpow(soil_temp / fc, beta);
+#endif
         const double soil_outflow = soil_q > soil_temp ? soil_temp : soil_q;
         sm = smax(0.0, sm + snow_outflow - soil_outflow - ae);
         // hbv_tank::step (hbv_tank.h:64-80)

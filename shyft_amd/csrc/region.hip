@@ -135,6 +135,13 @@ struct shyft_hip_region {
     // device
     dbuf<double> d_params, d_cellc, d_state, d_forcing, d_resp, d_state_series;
     dbuf<double> d_hand;  // pt_gs_k: [2][TW][n] gamma_snow -> flux hand-over of the split launch
+    // double-buffered forcing window (shyft_hip_prefetch_synthetic_forcing / shyft_hip_swap_forcing_window): the
+    // next window is generated on gen_stream (restricted to a few CUs) while the current one runs
+    dbuf<double> d_forcing_next;
+    hipStream_t gen_stream = nullptr;
+    int gen_cus = -1;
+    hipEvent_t ev_gen = nullptr;
+    size_t gen_w0 = SIZE_MAX;
     dbuf<int32_t> d_set_ix, d_err, d_doy, d_seg_cells, d_seg_off, d_sel;
     dbuf<int64_t> d_trel;
     dbuf<uint8_t> d_active;
@@ -504,6 +511,8 @@ void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->ev_mid) (void)hipEventDestroy(h->ev_mid);
+    if (h->ev_gen) (void)hipEventDestroy(h->ev_gen);
+    if (h->gen_stream) (void)hipStreamDestroy(h->gen_stream);
     if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -775,6 +784,62 @@ int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cel
                                            h->stream),
                   "synthetic_forcing");
         hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t w0_next,
+                                         int n_cus) {
+    if (!h) return fail(h, "shyft_hip_prefetch_synthetic_forcing: null handle");
+    return guarded(h, [&] {
+        if (h->T == 0 || h->TW == 0) throw std::runtime_error("prefetch_synthetic_forcing: no time axis");
+        if (w0_next + h->TW > h->T) throw std::runtime_error("prefetch_synthetic_forcing: window beyond the time axis");
+        if (!h->has_geo) throw std::runtime_error("prefetch_synthetic_forcing: geo_cell_data not set");
+        if (h->gen_w0 != SIZE_MAX) throw std::runtime_error("prefetch_synthetic_forcing: a prefetched window is pending");
+        if (!h->gen_stream || h->gen_cus != n_cus) {
+            if (h->gen_stream) {
+                hip_check(hipStreamSynchronize(h->gen_stream), "sync");
+                hip_check(hipStreamDestroy(h->gen_stream), "hipStreamDestroy");
+                h->gen_stream = nullptr;
+            }
+            int total = 0;
+            hip_check(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, h->device), "CU count");
+            if (n_cus > 0 && n_cus < total) {
+                // n_cus CUs spread evenly over the device (every XCD keeps most of its CUs for the run kernel)
+                std::vector<uint32_t> mask((size_t(total) + 31) / 32, 0u);
+                for (int k = 0; k < n_cus; ++k) {
+                    const int cu = int((long long)k * total / n_cus);
+                    mask[size_t(cu) / 32] |= 1u << (cu % 32);
+                }
+                hip_check(hipExtStreamCreateWithCUMask(&h->gen_stream, uint32_t(mask.size()), mask.data()),
+                          "hipExtStreamCreateWithCUMask");
+            } else {
+                hip_check(hipStreamCreateWithFlags(&h->gen_stream, hipStreamNonBlocking), "hipStreamCreate");
+            }
+            h->gen_cus = n_cus;
+        }
+        if (!h->ev_gen) hip_check(hipEventCreateWithFlags(&h->ev_gen, hipEventDisableTiming), "hipEventCreate");
+        h->d_forcing_next.alloc(h->d_forcing.n);
+        // the buffer was last read by a run on the region stream: the generator waits for that stream first
+        hip_check(hipEventRecord(h->ev_gen, h->stream), "record");
+        hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_gen, 0), "wait");
+        hip_check(launch_synthetic_forcing(h->d_forcing_next.p, h->TW, 0, h->TW, h->n, seed, cell_offset, w0_next,
+                                           h->d_alt.p, h->gen_stream),
+                  "synthetic_forcing (prefetch)");
+        hip_check(hipEventRecord(h->ev_gen, h->gen_stream), "record");
+        h->gen_w0 = w0_next;
+    });
+}
+
+int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next) {
+    if (!h) return fail(h, "shyft_hip_swap_forcing_window: null handle");
+    return guarded(h, [&] {
+        if (h->gen_w0 != w0_next) throw std::runtime_error("swap_forcing_window: no prefetched window at this step");
+        // later work on the region stream (the next run) waits for the generator, without a host wait
+        hip_check(hipStreamWaitEvent(h->stream, h->ev_gen, 0), "wait generator");
+        std::swap(h->d_forcing.p, h->d_forcing_next.p);
+        std::swap(h->d_forcing.n, h->d_forcing_next.n);
+        h->w0 = w0_next;
+        h->gen_w0 = SIZE_MAX;
     });
 }
 

@@ -161,6 +161,13 @@ class HipRegion:
     def synthetic_forcing(self, seed: int, step0: int, n: int, cell_offset: int = 0):
         self._chk(self._L.shyft_hip_synthetic_forcing(self.h, seed, cell_offset, step0, n))
 
+    def prefetch_synthetic_forcing(self, seed: int, w0_next: int, cell_offset: int = 0, n_cus: int = 8):
+        """Generate the next forcing window (rows w0_next .. w0_next + window) on a side stream of n_cus CUs."""
+        self._chk(self._L.shyft_hip_prefetch_synthetic_forcing(self.h, seed, cell_offset, w0_next, n_cus))
+
+    def swap_forcing_window(self, w0_next: int):
+        self._chk(self._L.shyft_hip_swap_forcing_window(self.h, w0_next))
+
     def run_cells(self, use_ncore: int = 0, start_step: int = 0, n_steps: int = 0):
         self._chk(self._L.shyft_hip_run_cells(self.h, int(use_ncore), int(start_step), int(n_steps)))
 
