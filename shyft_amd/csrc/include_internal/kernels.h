@@ -115,6 +115,10 @@ struct routing_args {
 hipError_t launch_route(const routing_args& a, const int* level_off, int n_levels, hipStream_t stream);
 
 // synthetic workload generator, fills [5][n][N] window rows
+// few-workgroup, non-temporal-store variant for generating beside a running kernel (n_blocks workgroups)
+hipError_t launch_synthetic_forcing_stream(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
+                                           uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
+                                           int n_blocks, hipStream_t stream);
 hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                     uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
                                     hipStream_t stream);

@@ -10,6 +10,27 @@
 
 namespace {
 
+// the prefetch variant (a few CUs, beside a running kernel): few long-lived workgroups striding over cells and rows,
+// so the side stream does not flood the workgroup dispatcher, and streaming (non-temporal) stores, so the 29 GB of
+// a window do not evict the running kernel's working set from L2
+__global__ __launch_bounds__(256) void synthetic_forcing_stream_kernel(double* __restrict__ forcing, size_t win_len,
+                                                                       size_t row0, size_t n_rows, size_t n_cells,
+                                                                       uint64_t seed, uint64_t cell_offset,
+                                                                       uint64_t step0, const double* __restrict__ zc) {
+#pragma clang fp contract(off)
+    for (size_t cell = blockIdx.x * (size_t)blockDim.x + threadIdx.x; cell < n_cells;
+         cell += (size_t)gridDim.x * blockDim.x) {
+        const double z = zc[cell];
+        const uint64_t gcell = cell_offset + cell;
+        for (size_t r = 0; r < n_rows; ++r) {
+            double v[5];
+            synth_values(seed, gcell, step0 + r, z, v);
+            const size_t o = (row0 + r) * n_cells + cell;
+            for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(v[k], &forcing[(size_t)k * win_len * n_cells + o]);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void synthetic_forcing_kernel(double* __restrict__ forcing, size_t win_len, size_t row0,
                                                                 size_t n_rows, size_t n_cells, uint64_t seed,
                                                                 uint64_t cell_offset, uint64_t step0,
@@ -37,6 +58,17 @@ hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0
     const unsigned gx = (unsigned)((n_cells + 255) / 256);
     unsigned gy = (unsigned)(n_rows < 64 ? n_rows : 64);
     hipLaunchKernelGGL(synthetic_forcing_kernel, dim3(gx, gy), dim3(256), 0, stream, forcing, win_len, row0, n_rows,
+                       n_cells, seed, cell_offset, step0, z);
+    return hipGetLastError();
+}
+
+hipError_t launch_synthetic_forcing_stream(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
+                                           uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
+                                           int n_blocks, hipStream_t stream) {
+    if (n_rows == 0 || n_cells == 0) return hipSuccess;
+    const size_t need = (n_cells + 255) / 256;
+    const unsigned gx = (unsigned)(need < (size_t)n_blocks ? need : (size_t)n_blocks);
+    hipLaunchKernelGGL(synthetic_forcing_stream_kernel, dim3(gx), dim3(256), 0, stream, forcing, win_len, row0, n_rows,
                        n_cells, seed, cell_offset, step0, z);
     return hipGetLastError();
 }

@@ -822,8 +822,9 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
         // the buffer was last read by a run on the region stream: the generator waits for that stream first
         hip_check(hipEventRecord(h->ev_gen, h->stream), "record");
         hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_gen, 0), "wait");
-        hip_check(launch_synthetic_forcing(h->d_forcing_next.p, h->TW, 0, h->TW, h->n, seed, cell_offset, w0_next,
-                                           h->d_alt.p, h->gen_stream),
+        const int blocks = 16 * (n_cus > 0 ? n_cus : 256);  // 4 workgroups of 4 waves per CU
+        hip_check(launch_synthetic_forcing_stream(h->d_forcing_next.p, h->TW, 0, h->TW, h->n, seed, cell_offset,
+                                                  w0_next, h->d_alt.p, blocks, h->gen_stream),
                   "synthetic_forcing (prefetch)");
         hip_check(hipEventRecord(h->ev_gen, h->gen_stream), "record");
         h->gen_w0 = w0_next;
