@@ -24,6 +24,10 @@ namespace {
 
 constexpr int KMAX = IDW_KMAX;
 
+#ifndef SHYFT_IDW_DZREG
+#define SHYFT_IDW_DZREG 1
+#endif
+
 __global__ __launch_bounds__(128) void idw_neighbours_kernel(idw_nb_args a) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n_cells) return;
@@ -126,13 +130,17 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
     const double dst_z = KIND == IDW_TEMPERATURE ? a.dst_xyz[3 * (size_t)j + 2] : 0.0;
     int nidx[KT];
     double nw[KT];
-    double naux[KIND == IDW_PRECIPITATION ? KT : 1];
+    // naux: precipitation pow(scale, dz/100); temperature (SHYFT_IDW_DZREG) d.z - s.z of each neighbour, the
+    // neighbour table's aux (the same subtraction of the same coordinates), held in registers instead of the
+    // per-row LDS read of s.z: K fewer LDS reads per cell-row (not with gradient_by_equation, whose instance has
+    // no VGPRs left for it at 2 waves per SIMD)
+    double naux[KIND == IDW_PRECIPITATION || (KIND == IDW_TEMPERATURE && SHYFT_IDW_DZREG && !BYEQ) ? KT : 1];
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
         const bool in = k < kept;
         nidx[k] = in ? a.idx[k * N + j] : 0;
         nw[k] = in ? a.w[k * N + j] : 0.0;
-        if (KIND == IDW_PRECIPITATION) naux[k] = in ? a.aux[k * N + j] : 0.0;
+        if (KIND == IDW_PRECIPITATION || (KIND == IDW_TEMPERATURE && SHYFT_IDW_DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
     }
     double* __restrict__ out = a.out;
     // Temperature fast path: when every source value of a row is finite (the common case) the gradient
@@ -313,7 +321,7 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
                     if (k >= kept) continue;
                     const double v = rowp[nidx[k]];
                     double tr;
-                    if (KIND == IDW_TEMPERATURE) tr = v + scale * (dst_z - src_z(nidx[k]));
+                    if (KIND == IDW_TEMPERATURE) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - src_z(nidx[k]));
                     else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
                     else if (KIND == IDW_RADIATION) tr = v * slope;
                     else tr = v;
@@ -328,7 +336,7 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
                 const double v = rowp[nidx[k]];
                 if (!__builtin_isfinite(v)) continue;
                 double tr;
-                if (KIND == IDW_TEMPERATURE) tr = v + scale * (dst_z - src_z(nidx[k]));
+                if (KIND == IDW_TEMPERATURE) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - src_z(nidx[k]));
                 else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
                 else if (KIND == IDW_RADIATION) tr = v * slope;
                 else tr = v;
