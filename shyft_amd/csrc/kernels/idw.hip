@@ -27,6 +27,9 @@ constexpr int KMAX = IDW_KMAX;
 #ifndef SHYFT_IDW_DZREG
 #define SHYFT_IDW_DZREG 1
 #endif
+#ifndef SHYFT_IDW_LDS_KB
+#define SHYFT_IDW_LDS_KB 60
+#endif
 
 __global__ __launch_bounds__(128) void idw_neighbours_kernel(idw_nb_args a) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -114,19 +117,22 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
     const int S = a.n_sources;
     const int kept = a.count[j];
     const double slope = KIND == IDW_RADIATION ? (a.slope ? a.slope[j] : 0.9) : 0.0;
-    // LDS layout: [src x | src y | src z] (temperature only) then the row tile
+    // LDS layout: [src x | src y | src z] (temperature with gradient_by_equation, or without SHYFT_IDW_DZREG) then
+    // the row tile; otherwise the coordinates are read from global memory where they are still needed (once per
+    // lane, and by the general scan of a row with a non-finite value)
+    constexpr bool COORDS = KIND == IDW_TEMPERATURE && (BYEQ || !SHYFT_IDW_DZREG);
     double* sxyz = smem;
-    double* tile = smem + (KIND == IDW_TEMPERATURE ? 3 * S : 0);
-    if (LDS && KIND == IDW_TEMPERATURE) {
+    double* tile = smem + (COORDS ? 3 * S : 0);
+    if (LDS && COORDS) {
         for (int i = threadIdx.x; i < S; i += blockDim.x) {
             sxyz[i] = a.src_xyz[3 * i];
             sxyz[S + i] = a.src_xyz[3 * i + 1];
             sxyz[2 * S + i] = a.src_xyz[3 * i + 2];
         }
     }
-    auto src_x = [&](int s) { return LDS ? sxyz[s] : a.src_xyz[3 * s]; };
-    auto src_y = [&](int s) { return LDS ? sxyz[S + s] : a.src_xyz[3 * s + 1]; };
-    auto src_z = [&](int s) { return LDS ? sxyz[2 * S + s] : a.src_xyz[3 * s + 2]; };
+    auto src_x = [&](int s) { return LDS && COORDS ? sxyz[s] : a.src_xyz[3 * s]; };
+    auto src_y = [&](int s) { return LDS && COORDS ? sxyz[S + s] : a.src_xyz[3 * s + 1]; };
+    auto src_z = [&](int s) { return LDS && COORDS ? sxyz[2 * S + s] : a.src_xyz[3 * s + 2]; };
     const double dst_z = KIND == IDW_TEMPERATURE ? a.dst_xyz[3 * (size_t)j + 2] : 0.0;
     int nidx[KT];
     double nw[KT];
@@ -152,8 +158,9 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
     int kmin = 0, kmax = 0;
     double inv[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     bool inv_ok = false;
+    double dz_fast = 0.0;  // src_z(nidx[kmax]) - src_z(nidx[kmin]): the fast path's gradient denominator per lane
     if (KIND == IDW_TEMPERATURE && LDS) {
-        __syncthreads();  // coordinates stored
+        if (COORDS) __syncthreads();  // coordinates stored
         double z_mn = 0, z_mx = 0;
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
@@ -163,6 +170,7 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
             else if (sz < z_mn) { z_mn = sz; kmin = k; }
             else if (sz > z_mx) { z_mx = sz; kmax = k; }
         }
+        dz_fast = src_z(nidx[kmax]) - src_z(nidx[kmin]);
         if (BYEQ && kept > 3) {
             double A[3][3];
             const double p0x = src_x(nidx[0]), p0y = src_y(nidx[0]), p0z = src_z(nidx[0]);
@@ -238,7 +246,7 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
                 }
                 if (!solved) {
                     if (kept > 1) {
-                        const double dzm = src_z(nidx[kmax]) - src_z(nidx[kmin]);
+                        const double dzm = dz_fast;
                         scale = dzm > 50.0 ? (row[nidx[kmax]] - row[nidx[kmin]]) / dzm : a.default_gradient;
                     } else {
                         scale = a.default_gradient;
@@ -383,9 +391,10 @@ hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
     if (a.n_cells == 0 || a.n_rows == 0) return hipSuccess;
     const dim3 grid((a.n_cells + 255) / 256), block(256);
     // LDS: the source coordinates (temperature) + a tile of source rows, up to 32 KB per workgroup
-    constexpr size_t LDS_BUDGET = 32 * 1024;
+    // (the kernels run at 2 waves per SIMD, 2 workgroups per CU: 60 KB each fits the 160 KB)
+    constexpr size_t LDS_BUDGET = SHYFT_IDW_LDS_KB * 1024;
     const size_t row_bytes = (size_t)a.n_sources * sizeof(double);
-    const size_t coord_bytes = a.kind == IDW_TEMPERATURE ? 3 * row_bytes : 0;
+    const size_t coord_bytes = a.kind == IDW_TEMPERATURE && (a.by_equation || !SHYFT_IDW_DZREG) ? 3 * row_bytes : 0;
     int lds_rows = row_bytes + coord_bytes <= LDS_BUDGET ? (int)((LDS_BUDGET - coord_bytes) / row_bytes) : 0;
     if (lds_rows > 64) lds_rows = 64;  // row_finite[] flags per tile
     if (lds_rows > a.n_rows) lds_rows = a.n_rows;
