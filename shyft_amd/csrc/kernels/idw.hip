@@ -28,7 +28,7 @@ constexpr int KMAX = IDW_KMAX;
 #define SHYFT_IDW_DZREG 1
 #endif
 #ifndef SHYFT_IDW_LDS_KB
-#define SHYFT_IDW_LDS_KB 60
+#define SHYFT_IDW_LDS_KB 32
 #endif
 
 __global__ __launch_bounds__(128) void idw_neighbours_kernel(idw_nb_args a) {
