@@ -13,6 +13,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/shyft_hip.h"
@@ -1230,7 +1231,9 @@ static void finish_run(shyft_hip_region* h) {
 // argument checks of region_model::run_cells (region_model.h:579-592), shared by the synchronous and the
 // asynchronous entry
 static void check_run_args(const shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {
-    const size_t ncore = 4096;  // the GPU path accepts any use_ncore the reference would
+    // the reference's ncore is the host's hardware_concurrency (region_model.h:280); 0 -> its minimum 4
+    size_t ncore = std::thread::hardware_concurrency();
+    if (ncore == 0) ncore = 4;
     if (use_ncore > 100 * ncore)
         throw std::runtime_error("illegal parameter value: use_ncore(" + std::to_string(use_ncore) +
                                  " is more than 100 time available physical cores: " + std::to_string(ncore));

@@ -174,3 +174,27 @@ def test_copy_state_then_set_state_on_source():
     finally:
         for r in regs:
             r.close()
+
+
+def test_use_ncore_check_uses_host_core_count():
+    """region_model.h:579-584 through the raw C ABI: use_ncore above 100 x the host's hardware_concurrency is
+    the reference's 'illegal parameter value' error; up to that it is accepted (and ignored by the GPU path)."""
+    import os
+    from shyft_amd.region import HipRegion, PT_GS_K
+    n = 64
+    geo, f, params, state = _region(n, 4)
+    r = HipRegion(PT_GS_K, n)
+    try:
+        r.set_geo(geo)
+        r.set_parameters(params)
+        r.set_time_axis(synthetic.T0_2015_US, HOUR, 4)
+        r.set_state(state)
+        for v in range(5):
+            r.set_forcing(v, 0, f[v])
+        hi = os.cpu_count() or 4  # hardware_concurrency lies between the affinity set and the online CPUs
+        lo = len(os.sched_getaffinity(0))
+        with pytest.raises(RuntimeError, match="more than 100 time available physical cores"):
+            r.run_cells(100 * hi + 1, 0, 4)
+        r.run_cells(100 * lo, 0, 4)
+    finally:
+        r.close()
