@@ -16,6 +16,11 @@
 #include "special.h"
 #include "../include_internal/layout.h"
 
+// SHYFT_GS_EXP2: the energy balance's two independent exps in one dexp2 call (gs step, below)
+#ifndef SHYFT_GS_EXP2
+#define SHYFT_GS_EXP2 1
+#endif
+
 namespace shyft_dev {
 
 constexpr double GS_TOL = 1.0e-10;  // gamma_snow::tol (gamma_snow.h:44)
@@ -260,7 +265,13 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
 
     const double sigma = 5.670373e-8;
     double effect = rad * (1.0 - albedo);
+#if SHYFT_GS_EXP2
+    // dpowr(vapour_pressure / T_k, 6.87e-2)'s exp and the sub-zero surface branch's exp in one dexp2 call
+    const dexp_pair gse = dexp2(6.87e-2 * dlog(vapour_pressure / T_k), 0.103 * T - 0.186);
+    effect += 0.98 * sigma * gse.a * dpow4(T_k);
+#else
     effect += 0.98 * sigma * dpowr(vapour_pressure / T_k, 6.87e-2) * dpow4(T_k);
+#endif
     if (T > 0.0 && snow < GS_TOL) effect += rain * T * 4180.0 / dt_s;
     if (T <= 0.0 && rain < GS_TOL) effect += snow * T * 2050.0 / dt_s;
 
@@ -272,7 +283,11 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
     if (sst > -GS_TOL)
         effect += turb * (T + 1.7 * (vapour_pressure - 6.12)) - P[PK_BB0];
     else
+#if SHYFT_GS_EXP2
+        effect += turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * gse.b)) -
+#else
         effect += turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * dexp(0.103 * T - 0.186))) -
+#endif
                   0.98 * sigma * dpow4(sst + 273.15);
 
     double delta_sh = -surface_heat;
@@ -448,9 +463,19 @@ __device__ inline double gs_solve_lwc(const gs_mid& m) {
 #define K_EXP_PASS
 #endif
 // kirchner.h:186-198
+// SHYFT_K_EXP2: both of kirchner_f's exps in one dexp2 call (exp(-ln_q) is evaluated even when g < 1e-30 does
+// not use it; the value is the same either way)
+#ifndef SHYFT_K_EXP2
+#define SHYFT_K_EXP2 1
+#endif
 __device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, double c2, double c3 K_EXP_ARG) {
+#if SHYFT_K_EXP2 && !SHYFT_K_FM
+    const dexp_pair ge = dexp2(c1 + c2 * ln_q + c3 * ln_q * ln_q, -ln_q);
+    return ge.a >= 1.e-30 ? ge.a * (p_minus_e * ge.b - 1.0) : 0.0;
+#else
     const double g = K_EXP(c1 + c2 * ln_q + c3 * ln_q * ln_q);
     return g >= 1.e-30 ? g * (p_minus_e * K_EXP(-ln_q) - 1.0) : 0.0;
+#endif
 }
 
 // kirchner::calculator::step with trapezoidal_average (kirchner.h:23-53, 213-235).
@@ -507,7 +532,9 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         attempts = 0;
         t_old = t;
         t = t + dt;
-        if (err < 0.5) {
+        // the grown step size only matters if the loop goes on (dt is dead once t reaches t1: every call starts
+        // from dt = t1), so the log + exp of the controller are skipped on the call's last step
+        if (err < 0.5 && t < t1) {
             const double e2 = smax(0.00032, err);  // dpow(5.0, -5.0)
             dt = dt * (9.0 / 10.0 * K_EXP(-1.0 / 5.0 * dlog(e2)));  // dpowr(e2, -1/5)
         }

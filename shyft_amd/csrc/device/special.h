@@ -43,11 +43,62 @@ __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b 
 #ifndef SHYFT_DM_INLINE_POW
 #define SHYFT_DM_INLINE_POW __noinline__
 #endif
+// SHYFT_DM_SGPR: the out-of-line exp / log take their polynomial coefficients as SGPR operands of v_fma_f64
+// (s_mov pairs on the scalar unit) instead of the compiler's v_mov_b32 pair per coefficient (dm_sgpr.h)
+#ifndef SHYFT_DM_SGPR
+#define SHYFT_DM_SGPR 0
+#endif
+#if SHYFT_DM_SGPR
+}  // namespace shyft_dev
+#include "dm_sgpr.h"
+namespace shyft_dev {
+__device__ SHYFT_DM_INLINE double dexp(double x) { return dm_exp_s(x); }
+#else
 __device__ SHYFT_DM_INLINE double dexp(double x) { return detmath::exp(x); }
+#endif
 #ifndef SHYFT_DM_INLINE_LOG
 #define SHYFT_DM_INLINE_LOG SHYFT_DM_INLINE
 #endif
+#if SHYFT_DM_SGPR
+__device__ SHYFT_DM_INLINE_LOG double dlog(double x) { return dm_log_s(x); }
+#else
 __device__ SHYFT_DM_INLINE_LOG double dlog(double x) { return detmath::log(x); }
+#endif
+// two exps in one out-of-line call: the two Horner chains interleave (each one's fma latency hidden behind the
+// other's), where two calls would run them back to back; the same bits as two dexp calls
+struct dexp_pair {
+    double a, b;
+};
+__device__ __noinline__ dexp_pair dexp2(double x, double y) {
+    dexp_pair r;
+    if (__builtin_fabs(x) <= 708.0 && __builtin_fabs(y) <= 708.0) {
+#pragma clang fp contract(off)
+        // detmath::exp_poly on both arguments, step by step side by side
+        const double tx = x * 1.4426950408889634 + 6755399441055744.0, ty = y * 1.4426950408889634 + 6755399441055744.0;
+        const double kx = tx - 6755399441055744.0, ky = ty - 6755399441055744.0;
+        double rx = __builtin_fma(-kx, 6.93147180369123816490e-01, x), ry = __builtin_fma(-ky, 6.93147180369123816490e-01, y);
+        rx = __builtin_fma(-kx, 1.90821492927058770002e-10, rx);
+        ry = __builtin_fma(-ky, 1.90821492927058770002e-10, ry);
+        const double C[13] = {1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08,
+                              2.7557319223985893e-07, 2.7557319223985888e-06, 2.4801587301587302e-05,
+                              1.9841269841269841e-04, 1.3888888888888889e-03, 8.3333333333333333e-03,
+                              4.1666666666666664e-02, 1.6666666666666666e-01, 0.5, 1.0};
+        double px = C[0], py = C[0];
+#pragma unroll
+        for (int i = 1; i < 13; ++i) {
+            px = __builtin_fma(px, rx, C[i]);
+            py = __builtin_fma(py, ry, C[i]);
+        }
+        px = __builtin_fma(px, rx, 1.0);
+        py = __builtin_fma(py, ry, 1.0);
+        r.a = __builtin_ldexp(px, (int)kx);
+        r.b = __builtin_ldexp(py, (int)ky);
+    } else {
+        r.a = detmath::exp(x);
+        r.b = detmath::exp(y);
+    }
+    return r;
+}
 __device__ SHYFT_DM_INLINE_POW double dpow(double x, double y) { return detmath::pow(x, y); }
 __device__ __noinline__ double dlgamma(double x) { return detmath::lgamma(x); }
 // structured powers (detmath::pow4 / pow8 / powr, the oracle's OPOW4 / OPOW8 / OPOWR)

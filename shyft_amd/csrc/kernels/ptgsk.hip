@@ -29,6 +29,10 @@ using namespace shyft_dev;
 #ifndef SHYFT_BRENT_LEAN
 #define SHYFT_BRENT_LEAN 0
 #endif
+// Priestley-Taylor's saturation-pressure exp and actual_evapotranspiration's exp in one dexp2 call
+#ifndef SHYFT_PT_AE2
+#define SHYFT_PT_AE2 1
+#endif
 #if SHYFT_BRENT_LEAN
 #define GS_BRENT_JOB gs_corr_lwc_lean
 #else
@@ -224,8 +228,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
         m.need = false;
         m.done = true;
         LOAD_GCELL();
+#ifndef SHYFT_ABLATE_SNOW
         if (valid)
             gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc, carry);
+#endif
         PROF_MARK(0);  // forcing + gs_front
         double z = 0.0;
         if (COMPACT) {
@@ -284,7 +290,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
         if (!valid) continue;
         double gs_sca, gs_storage, gs_outflow;
         LOAD_GCELL();
+#ifdef SHYFT_ABLATE_SNOW  // instruction-budget ablation only (wrong results): no snow routine at all
+        gs_sca = 0.0; gs_storage = 0.0; gs_outflow = prec + 0.0 * z;
+#else
         gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc, carry);
+#endif
         PROF_MARK(3);  // gs_back
 
         // glacier_melt::step (glacier_melt.h:47-52)
@@ -292,8 +302,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
         double gm_melt_m3s = 0.0;
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
+#if SHYFT_PT_AE2
+        double ae_exp;
+        const double pot_evap =
+            pt_pot_evap_exp(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum, -q * 3.0 / P[PK_AE_SCALE], ae_exp) * 3600.0;
+        const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(gs_sca, glacier_fraction));
+#else
         const double pot_evap = pt_pot_evap(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum) * 3600.0;
         const double ae = pot_evap * (1.0 - dexp(-q * 3.0 / P[PK_AE_SCALE])) * (1.0 - smax(gs_sca, glacier_fraction));
+#endif
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         PROF_MARK(4);  // glacier, PT, AE
         double q_avg;
@@ -549,8 +566,15 @@ __global__ __launch_bounds__(BLOCK, SHYFT_FLUX_WAVES) void ptgsk_flux_kernel(con
         double gm_melt_m3s = 0.0;
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = P[PK_DTF] * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
+#if SHYFT_PT_AE2
+        double ae_exp;
+        const double pot_evap =
+            pt_pot_evap_exp(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum, -q * 3.0 / P[PK_AE_SCALE], ae_exp) * 3600.0;
+        const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(gs_sca, glacier_fraction));
+#else
         const double pot_evap = pt_pot_evap(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum) * 3600.0;
         const double ae = pot_evap * (1.0 - dexp(-q * 3.0 / P[PK_AE_SCALE])) * (1.0 - smax(gs_sca, glacier_fraction));
+#endif
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         double q_avg;
         if (!kirchner_step(q, q_avg, gs_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,

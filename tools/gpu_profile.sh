@@ -12,19 +12,23 @@ R=$(pwd)
 ARGS=${BENCH_ARGS:---gpus 1 --steps 20 --warmup 5}
 ROUND=${ROUND:-r03}
 KERNEL=${KERNEL:-ptgsk_run_kernel}
+O=$R/gpurun_out/${TAG:-.}; mkdir -p $O   # TAG: one sub-directory per workload when a call profiles several
 cd /tmp && export TMPDIR=/tmp
 run() {  # name, rocprofv3 args...
     local name=$1; shift
-    rm -rf $R/gpurun_out/prof_$name
-    timeout -k 10 400 rocprofv3 "$@" -d $R/gpurun_out/prof_$name -o run --output-format csv -- \
-        python3 $R/bench.py $ARGS > $R/gpurun_out/prof_$name.log 2>&1 \
-        || { echo "PROF $name FAILED"; tail -20 $R/gpurun_out/prof_$name.log; exit 1; }
+    rm -rf $O/prof_$name
+    timeout -k 10 400 rocprofv3 "$@" -d $O/prof_$name -o run --output-format csv -- \
+        python3 $R/bench.py $ARGS > $O/prof_$name.log 2>&1 \
+        || { echo "PROF $name FAILED"; tail -20 $O/prof_$name.log; exit 1; }
     echo "prof $name ok"
 }
 run trace --kernel-trace --stats
 run fetch --kernel-trace --pmc FETCH_SIZE
 run write --kernel-trace --pmc WRITE_SIZE
-run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
+run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE
 cd $R
-python3 tools/pmc_summary.py --kernel $KERNEL --round $ROUND --bench-args "$ARGS" || exit 1
-find gpurun_out -path "*prof_*" -name "*.csv" | sort
+echo "$ARGS" > $O/bench_args.txt
+echo "$KERNEL" > $O/kernel.txt
+# the summary is written here after the call (profiles/ does not travel back from the box):
+#   python3 tools/pmc_summary.py --kernel $KERNEL --round $ROUND --bench-args "$ARGS" --base $O
+find $O -path "*prof_*" -name "*.csv" | sort
