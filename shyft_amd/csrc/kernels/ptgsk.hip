@@ -27,7 +27,7 @@ using namespace shyft_dev;
 // the Brent job of the solving wavefront: gs_corr_lwc_lean (device/gs_brent.h, the same arithmetic in fewer
 // instructions) or the reference-shaped gs_corr_lwc
 #ifndef SHYFT_BRENT_LEAN
-#define SHYFT_BRENT_LEAN 0
+#define SHYFT_BRENT_LEAN 1
 #endif
 // Priestley-Taylor's saturation-pressure exp and actual_evapotranspiration's exp in one dexp2 call
 #ifndef SHYFT_PT_AE2
