@@ -15,6 +15,11 @@
 #include "special.h"
 #include "../include_internal/layout.h"
 
+// SHYFT_HBV_INT2: the snow step's two integrals in one walk over the bins (hbv_integrate0_2)
+#ifndef SHYFT_HBV_INT2
+#define SHYFT_HBV_INT2 1
+#endif
+
 namespace shyft_dev {
 
 #ifndef HBV_MB_OVERRIDE
@@ -83,6 +88,55 @@ __device__ __forceinline__ double hbv_integrate0(const double (&f)[NB], const do
         }
     }
     return area;
+}
+
+// hbv_integrate0 of two functions over the same abscissae and limits (the snow step's swe = integral of sp + integral
+// of sw): one walk over the bins; each area is accumulated exactly as its own hbv_integrate0 call would
+template <int NB>
+__device__ __forceinline__ void hbv_integrate0_2(const double (&f)[NB], const double (&g)[NB], const double (&x)[NB],
+                                                 int n, double b, bool f_b_is_zero, double& area_f, double& area_g) {
+    const double a = 0.0;
+    int left = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+        if (i < n && left == i && a > x[i]) left = i + 1;
+    double f_l, g_l;
+    if (fabs(a - hsel(x, left)) > 1.0e-8 && left > 0) {
+        --left;
+        const double xl = hsel(x, left), xr = hsel(x, left + 1);
+        const double fl = hsel(f, left), fr = hsel(f, left + 1);
+        const double gl = hsel(g, left), gr = hsel(g, left + 1);
+        f_l = (fr - fl) / (xr - xl) * (a - xl) + fl;
+        g_l = (gr - gl) / (xr - xl) * (a - xl) + gl;
+    } else {
+        f_l = hsel(f, left);
+        g_l = hsel(g, left);
+    }
+    double af = 0.0, ag = 0.0, x_l = a;
+    bool done = false;
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) {
+        if (!done && i >= left && i < n - 1) {
+            if (b >= x[i + 1]) {
+                af += 0.5 * (f_l + f[i + 1]) * (x[i + 1] - x_l);
+                ag += 0.5 * (g_l + g[i + 1]) * (x[i + 1] - x_l);
+                x_l = x[i + 1];
+                f_l = f[i + 1];
+                g_l = g[i + 1];
+            } else {
+                if (!f_b_is_zero) {
+                    af += (f_l + 0.5 * (f[i + 1] - f_l) / (x[i + 1] - x_l) * (b - x_l)) * (b - x_l);
+                    ag += (g_l + 0.5 * (g[i + 1] - g_l) / (x[i + 1] - x_l) * (b - x_l)) * (b - x_l);
+                } else {
+                    af += 0.5 * f_l * (b - x_l);
+                    ag += 0.5 * g_l * (b - x_l);
+                }
+                done = true;
+            }
+        }
+    }
+    area_f = af;
+    area_g = ag;
 }
 
 // hbv_snow::state::distribute -> distribute_snow (hbv_snow.h:95-99, hbv_snow_common.h:47-66)
@@ -215,8 +269,15 @@ __device__ inline double hbv_snow_step(const hbv_snow_par_t<NB>& p, double (&sp)
         swe = 0.0;
     } else {
         const bool f_is_zero = sca >= 1.0 ? false : true;
+#if SHYFT_HBV_INT2
+        double a_sp, a_sw;
+        hbv_integrate0_2(sp, sw, p.I, nb, sca, f_is_zero, a_sp, a_sw);
+        swe = a_sp;
+        swe += a_sw;
+#else
         swe = hbv_integrate0(sp, p.I, nb, sca, f_is_zero);
         swe += hbv_integrate0(sw, p.I, nb, sca, f_is_zero);
+#endif
     }
     if (total_water < swe) {
         if (total_water - swe < -1.0e-6) err = ERR_NEGATIVE_OUTFLOW;  // the reference throws (hbv_snow.h:259-263)

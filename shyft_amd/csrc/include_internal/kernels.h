@@ -175,7 +175,25 @@ struct idw_gather_args {
     const int32_t* count;
     const uint8_t* active;     // catchment calculation filter or null
     double* out;               // [n_rows][N] (a forcing window slice)
+    // wave-union tables (idw_wave_union): when set, the gather reads each neighbour through its wavefront's
+    // compacted station list instead of a row tile of every source
+    const int32_t* wu;         // [ceil(N/64)][64] stations of the wavefront's union (lanes >= union size: 0)
+    const int32_t* wn;         // [ceil(N/64)] union size
+    const uint32_t* lidx;      // [ceil(K/4)][N] the neighbours' positions in the union, 4 bytes per word
 };
+
+// per wavefront of 64 cells: the union of their neighbour lists (<= 64 stations) and every neighbour's position in
+// it; *overflow = 1 if some wavefront needs more than 64 stations (the gather then keeps the row-tile path)
+struct idw_union_args {
+    int n_cells, max_members;
+    const int32_t* idx;
+    const int32_t* count;
+    int32_t* wu;
+    int32_t* wn;
+    uint32_t* lidx;
+    int32_t* overflow;
+};
+hipError_t launch_idw_wave_union(const idw_union_args& a, hipStream_t stream);
 
 hipError_t launch_idw_neighbours(const idw_nb_args& a, hipStream_t stream);
 hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream);

@@ -205,14 +205,22 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         }
         const double prec = prec_raw * p_corr;
         if (SS) collect_state(wi);
+#ifdef SHYFT_ABLATE_HSNOW  // instruction-budget ablation only (wrong results): no snow routine
+        const double snow_outflow = prec + 0.0 * temp;
+#else
         const double snow_outflow =
             hbv_snow_step(sp_par, sp, sw, swe, sca, a.step_in_days, a.dt_hours, prec, temp, err);
+#endif
         // glacier_melt::step (glacier_melt.h:47-52) on the snow covered area after the snow step
         const double sca_area = cell_area_m2 * sca;
         double gm_melt_m3s = 0.0;
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
+#ifdef SHYFT_ABLATE_PT  // instruction-budget ablation only (wrong results): no Priestley-Taylor
+        const double pot_evap = (rad * 1e-4 + rel_hum * 1e-5 + temp * 1e-6) * pt_alpha;
+#else
         const double pot_evap = pt_pot_evap(pt_albedo, pt_alpha, temp, rad, rel_hum) * 3600.0;
+#endif
         // hbv_actual_evapotranspiration::calculate_step (hbv_actual_evapotranspiration.h:32-38)
         const double snow_fraction = smax(sca, glacier_fraction);
         const double ae = (1.0 - snow_fraction) * (sm < lp ? pot_evap * (sm / lp) : pot_evap);

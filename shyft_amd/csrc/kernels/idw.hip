@@ -27,6 +27,10 @@ constexpr int KMAX = IDW_KMAX;
 #ifndef SHYFT_IDW_DZREG
 #define SHYFT_IDW_DZREG 1
 #endif
+// SHYFT_IDW_WAVE: gathers through the wavefront's union of neighbour stations when every wavefront's union fits 64
+#ifndef SHYFT_IDW_WAVE
+#define SHYFT_IDW_WAVE 1
+#endif
 #ifndef SHYFT_IDW_LDS_KB
 #define SHYFT_IDW_LDS_KB 32
 #endif
@@ -370,6 +374,299 @@ __global__ __launch_bounds__(256) void idw_gather_kernel(idw_gather_args a, int 
 }
 
 
+// ------------------------------------------------------------------ wavefront-union gathers
+// A wavefront's 64 cells are neighbours on the ground, so their neighbour lists draw on a few dozen stations. The
+// union kernel lists those stations once per wavefront (<= 64) and stores each neighbour as its position in that
+// list (one byte). The gather then has lane u fetch station u's value of a row (one gathered load from L2 per lane
+// and row, prefetched several rows ahead) into a 64-entry LDS slot of its wavefront, and every neighbour read is an
+// LDS read of that slot: a few dozen distinct addresses in 128 consecutive dwords, where the row tile spread them
+// over every source's 8 bytes (bank conflicts bound the tile kernel). No workgroup barriers: the wavefronts are
+// independent. Values, weights and the order of every sum are the tile kernel's, so the results are the same bits.
+__global__ __launch_bounds__(64) void idw_wave_union_kernel(idw_union_args a) {
+    const int N = a.n_cells;
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * 64 + lane;
+    const int kept = j < N ? a.count[j] : 0;
+    int nid[IDW_KMAX];
+    int loc[IDW_KMAX];
+#pragma unroll
+    for (int k = 0; k < IDW_KMAX; ++k) {
+        nid[k] = k < kept ? a.idx[(size_t)k * N + j] : -1;
+        loc[k] = 255;
+    }
+    int cnt = 0, mine = 0;
+    bool over = false;
+    for (;;) {
+        int cand = -1;
+#pragma unroll
+        for (int k = IDW_KMAX - 1; k >= 0; --k)
+            if (nid[k] >= 0 && loc[k] == 255) cand = nid[k];
+        const unsigned long long b = __ballot(cand >= 0);
+        if (b == 0ull) break;
+        if (cnt == 64) {
+            over = true;
+            break;
+        }
+        const int s = __shfl(cand, __ffsll((long long)b) - 1, 64);
+#pragma unroll
+        for (int k = 0; k < IDW_KMAX; ++k)
+            if (nid[k] == s) loc[k] = cnt;
+        if (lane == cnt) mine = s;
+        ++cnt;
+    }
+    a.wu[(size_t)blockIdx.x * 64 + lane] = (!over && lane < cnt) ? mine : 0;
+    if (lane == 0) {
+        a.wn[blockIdx.x] = over ? -1 : cnt;
+        if (over) atomicMax(a.overflow, 1);
+    }
+    if (j < N) {
+        const int nq = (a.max_members + 3) / 4;
+#pragma unroll
+        for (int q = 0; q < IDW_KMAX / 4; ++q)
+            if (q < nq)
+                a.lidx[(size_t)q * N + j] = (uint32_t)loc[4 * q] | ((uint32_t)loc[4 * q + 1] << 8) |
+                                            ((uint32_t)loc[4 * q + 2] << 16) | ((uint32_t)loc[4 * q + 3] << 24);
+    }
+}
+
+#ifndef SHYFT_IDW_WAVE_OCC
+#define SHYFT_IDW_WAVE_OCC 1
+#endif
+template <int KT, int KIND, bool BYEQ>
+__global__ __launch_bounds__(256, SHYFT_IDW_WAVE_OCC) void idw_wave_gather_kernel(idw_gather_args a) {
+    constexpr int P = 4;  // source rows in flight per lane
+    constexpr bool TEMP = KIND == IDW_TEMPERATURE;
+    __shared__ double vslot[4][2][64];                 // each wavefront's union values of a row (double-buffered)
+    __shared__ double zslot[TEMP ? 4 : 1][64];         // the union's z
+    __shared__ double xslot[BYEQ ? 4 : 1][64], yslot[BYEQ ? 4 : 1][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int wave = j >> 6;
+    const int NC = a.n_cells;
+    if (wave * 64 >= NC) return;  // a whole wavefront past the cells (wave-uniform; no barriers below)
+    const size_t N = (size_t)NC;
+    const bool in_range = j < NC;
+    const bool lane_on = in_range && !(a.active && !a.active[j]);
+    const int S = a.n_sources;
+    const int un = a.wn[wave];
+    const int su = lane < un ? a.wu[(size_t)wave * 64 + lane] : 0;
+    if (TEMP) zslot[wv][lane] = a.src_xyz[3 * (size_t)su + 2];
+    if (BYEQ) {
+        xslot[BYEQ ? wv : 0][lane] = a.src_xyz[3 * (size_t)su];
+        yslot[BYEQ ? wv : 0][lane] = a.src_xyz[3 * (size_t)su + 1];
+    }
+    const int kept = in_range ? a.count[j] : 0;
+    const double slope = KIND == IDW_RADIATION ? (in_range ? (a.slope ? a.slope[j] : 0.9) : 0.0) : 0.0;
+    const double dst_z = TEMP && in_range ? a.dst_xyz[3 * (size_t)j + 2] : 0.0;
+    uint32_t lw[(KT + 3) / 4];
+#pragma unroll
+    for (int q = 0; q < (KT + 3) / 4; ++q) lw[q] = 4 * q < kept ? a.lidx[(size_t)q * N + j] : 0u;
+    auto L = [&](int k) { return (int)((lw[k >> 2] >> (8 * (k & 3))) & 0xffu); };
+    double nw[KT];
+    double naux[KIND == IDW_PRECIPITATION || (TEMP && SHYFT_IDW_DZREG && !BYEQ) ? KT : 1];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+        const bool in = k < kept;
+        nw[k] = in ? a.w[k * N + j] : 0.0;
+        if (KIND == IDW_PRECIPITATION || (TEMP && SHYFT_IDW_DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
+    }
+    const double* zs = zslot[TEMP ? wv : 0];
+    const double* xs = xslot[BYEQ ? wv : 0];
+    const double* ys = yslot[BYEQ ? wv : 0];
+    __builtin_amdgcn_wave_barrier();
+    // the gradient's fixed geometry (idw_gather_body's fast path, from the union's coordinates)
+    int kmin = 0, kmax = 0;
+    double inv[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    bool inv_ok = false;
+    double dz_fast = 0.0;
+    if (TEMP) {
+        double z_mn = 0, z_mx = 0;
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            if (k >= kept) continue;
+            const double sz = zs[L(k)];
+            if (k == 0) { z_mn = z_mx = sz; kmin = kmax = 0; }
+            else if (sz < z_mn) { z_mn = sz; kmin = k; }
+            else if (sz > z_mx) { z_mx = sz; kmax = k; }
+        }
+        if (kept > 0) dz_fast = zs[L(kmax)] - zs[L(kmin)];
+        if (BYEQ && kept > 3) {
+            double A[3][3];
+            const double p0x = xs[L(0)], p0y = ys[L(0)], p0z = zs[L(0)];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                A[q][0] = xs[L(q + 1)] - p0x; A[q][1] = ys[L(q + 1)] - p0y; A[q][2] = zs[L(q + 1)] - p0z;
+            }
+            const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) -
+                               A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                               A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+            if (fabs(det) > 0.0 && __builtin_isfinite(det)) {
+                inv_ok = true;
+                inv[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+                inv[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+                inv[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+                inv[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+                inv[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+                inv[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+                inv[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+                inv[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+                inv[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+            }
+        }
+    }
+    double sw_all = 0.0;
+#pragma unroll
+    for (int k = 0; k < KT; ++k)
+        if (k < kept) sw_all += nw[k];
+    // every cell of the wavefront has KT neighbours (lanes past the cells read slot 0 with weight 0, unused)
+    const bool full = __ballot(in_range && kept != KT) == 0ull;
+    const double* __restrict__ src = a.src_values;
+    const int R = a.n_rows;
+    double pv[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) pv[p] = (lane < un && p < R) ? src[(size_t)p * S + su] : 0.0;
+    double* __restrict__ out = a.out;
+    for (int r = 0; r < R; ++r) {
+        const double v_in = pv[0];
+#pragma unroll
+        for (int p = 0; p + 1 < P; ++p) pv[p] = pv[p + 1];
+        pv[P - 1] = (lane < un && r + P < R) ? src[(size_t)(r + P) * S + su] : 0.0;
+        double* row = vslot[wv][r & 1];
+        row[lane] = v_in;
+        const bool fin = __ballot(lane < un && !__builtin_isfinite(v_in)) == 0ull;
+        __builtin_amdgcn_wave_barrier();
+        double scale = 1.0;
+        if (TEMP && fin) {
+            bool solved = false;
+            if (BYEQ && inv_ok) {
+                const double t0 = row[L(0)];
+                const double b0 = row[L(1)] - t0, b1 = row[L(2)] - t0, b2 = row[L(3)] - t0;
+                const double x0 = inv[0][0] * b0 + inv[0][1] * b1 + inv[0][2] * b2;
+                const double x1 = inv[1][0] * b0 + inv[1][1] * b1 + inv[1][2] * b2;
+                const double x2 = inv[2][0] * b0 + inv[2][1] * b1 + inv[2][2] * b2;
+                if (__builtin_isfinite(x0) && __builtin_isfinite(x1) && __builtin_isfinite(x2)) {
+                    scale = x2;
+                    solved = true;
+                }
+            }
+            if (!solved) {
+                if (kept > 1) scale = dz_fast > 50.0 ? (row[L(kmax)] - row[L(kmin)]) / dz_fast : a.default_gradient;
+                else scale = a.default_gradient;
+            }
+        } else if (TEMP) {
+            // temperature_gradient_scale_computer over the valid neighbours (inverse_distance.h:305-330)
+            int n = 0;
+            double z_mn = 0, z_mx = 0, t_mn = 0, t_mx = 0;
+            double p0x = 0, p0y = 0, p0z = 0, t0 = 0;
+            double A[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, b[3] = {0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < KT; ++k) {
+                if (k >= kept) continue;
+                const double v = row[L(k)];
+                if (!__builtin_isfinite(v)) continue;
+                const double sz = zs[L(k)];
+                if (n == 0) {
+                    z_mn = z_mx = sz;
+                    t_mn = t_mx = v;
+                } else if (sz < z_mn) {
+                    z_mn = sz; t_mn = v;
+                } else if (sz > z_mx) {
+                    z_mx = sz; t_mx = v;
+                }
+                if (BYEQ) {
+                    const double sx = xs[L(k)], sy = ys[L(k)];
+                    if (n == 0) { p0x = sx; p0y = sy; p0z = sz; t0 = v; }
+                    else if (n == 1) { A[0][0] = sx - p0x; A[0][1] = sy - p0y; A[0][2] = sz - p0z; b[0] = v - t0; }
+                    else if (n == 2) { A[1][0] = sx - p0x; A[1][1] = sy - p0y; A[1][2] = sz - p0z; b[1] = v - t0; }
+                    else if (n == 3) { A[2][0] = sx - p0x; A[2][1] = sy - p0y; A[2][2] = sz - p0z; b[2] = v - t0; }
+                }
+                ++n;
+            }
+            bool solved = false;
+            if (BYEQ && n > 3) {
+                const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) -
+                                   A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                                   A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+                if (fabs(det) > 0.0 && __builtin_isfinite(det)) {
+                    const double i20 = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+                    const double i21 = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+                    const double i22 = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+                    const double i00 = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+                    const double i01 = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+                    const double i02 = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+                    const double i10 = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+                    const double i11 = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+                    const double i12 = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+                    const double x0 = i00 * b[0] + i01 * b[1] + i02 * b[2];
+                    const double x1 = i10 * b[0] + i11 * b[1] + i12 * b[2];
+                    const double x2 = i20 * b[0] + i21 * b[1] + i22 * b[2];
+                    if (__builtin_isfinite(x0) && __builtin_isfinite(x1) && __builtin_isfinite(x2)) {
+                        scale = x2;
+                        solved = true;
+                    }
+                }
+            }
+            if (!solved) {
+                if (n > 1) {
+                    const double dzm = z_mx - z_mn;
+                    scale = dzm > 50.0 ? (t_mx - t_mn) / dzm : a.default_gradient;
+                } else {
+                    scale = a.default_gradient;
+                }
+            }
+        }
+        double sum_weights = 0.0, sum_weight_value = 0.0;
+        if (fin && full) {
+            // every lane of the wavefront has KT neighbours: straight-line sum, reads issued back to back
+#pragma unroll
+            for (int k = 0; k < KT; ++k) {
+                const int l = L(k);
+                const double v = row[l];
+                double tr;
+                if (TEMP) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
+                else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
+                else if (KIND == IDW_RADIATION) tr = v * slope;
+                else tr = v;
+                sum_weight_value += nw[k] * tr;
+            }
+            if (lane_on) out[(size_t)r * N + j] = sum_weight_value / sw_all;
+            continue;
+        }
+        if (fin) {
+            // branch-free over the KT slots (a slot past the lane's count reads a valid LDS word and is not added):
+            // the LDS reads issue back to back instead of one read-and-wait per neighbour
+#pragma unroll
+            for (int k = 0; k < KT; ++k) {
+                const int l = L(k) & 63;
+                const double v = row[l];
+                double tr;
+                if (TEMP) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
+                else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
+                else if (KIND == IDW_RADIATION) tr = v * slope;
+                else tr = v;
+                const double acc = sum_weight_value + nw[k] * tr;
+                sum_weight_value = k < kept ? acc : sum_weight_value;
+            }
+            if (lane_on) out[(size_t)r * N + j] = sum_weight_value / sw_all;
+            continue;
+        }
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            if (k >= kept) continue;
+            const double v = row[L(k)];
+            if (!__builtin_isfinite(v)) continue;
+            double tr;
+            if (TEMP) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - zs[L(k)]);
+            else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
+            else if (KIND == IDW_RADIATION) tr = v * slope;
+            else tr = v;
+            sum_weight_value += nw[k] * tr;
+            sum_weights += nw[k];
+        }
+        if (lane_on) out[(size_t)r * N + j] = sum_weight_value / sum_weights;
+    }
+}
+
 // single temperature source: copied to every calculated cell (region_model.h:470-481)
 __global__ void copy_source_kernel(const double* __restrict__ v, int n_rows, int n_cells, const uint8_t* __restrict__ active,
                                    double* __restrict__ out) {
@@ -411,6 +708,33 @@ hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
         else                                                                                                         \
             hipLaunchKernelGGL((idw_gather_kernel<IDW_KMAX, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);  \
     } while (0)
+#if SHYFT_IDW_WAVE
+    if (a.wu && a.wn && a.lidx) {
+        const dim3 wgrid((a.n_cells + 255) / 256);
+#define SHYFT_IDW_WLAUNCH(KIND_, BYEQ_)                                                                              \
+    do {                                                                                                             \
+        if (a.max_members <= 8)                                                                                      \
+            hipLaunchKernelGGL((idw_wave_gather_kernel<8, KIND_, BYEQ_>), wgrid, block, 0, stream, a);               \
+        else if (a.max_members <= 12)                                                                                \
+            hipLaunchKernelGGL((idw_wave_gather_kernel<12, KIND_, BYEQ_>), wgrid, block, 0, stream, a);              \
+        else if (a.max_members <= 20)                                                                                \
+            hipLaunchKernelGGL((idw_wave_gather_kernel<20, KIND_, BYEQ_>), wgrid, block, 0, stream, a);              \
+        else                                                                                                         \
+            hipLaunchKernelGGL((idw_wave_gather_kernel<IDW_KMAX, KIND_, BYEQ_>), wgrid, block, 0, stream, a);        \
+    } while (0)
+        switch (a.kind) {
+            case IDW_TEMPERATURE:
+                if (a.by_equation) SHYFT_IDW_WLAUNCH(IDW_TEMPERATURE, true);
+                else SHYFT_IDW_WLAUNCH(IDW_TEMPERATURE, false);
+                break;
+            case IDW_PRECIPITATION: SHYFT_IDW_WLAUNCH(IDW_PRECIPITATION, false); break;
+            case IDW_RADIATION: SHYFT_IDW_WLAUNCH(IDW_RADIATION, false); break;
+            default: SHYFT_IDW_WLAUNCH(IDW_WIND_SPEED, false); break;
+        }
+#undef SHYFT_IDW_WLAUNCH
+        return hipGetLastError();
+    }
+#endif
     switch (a.kind) {
         case IDW_TEMPERATURE:
             if (a.by_equation) SHYFT_IDW_LAUNCH(IDW_TEMPERATURE, true);
@@ -421,6 +745,13 @@ hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
         default: SHYFT_IDW_LAUNCH(IDW_WIND_SPEED, false); break;  // wind speed and rel_hum: plain mean
     }
 #undef SHYFT_IDW_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_idw_wave_union(const idw_union_args& a, hipStream_t stream) {
+    if (a.n_cells == 0) return hipSuccess;
+    if (a.max_members < 1 || a.max_members > IDW_KMAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(idw_wave_union_kernel, dim3((a.n_cells + 63) / 64), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 

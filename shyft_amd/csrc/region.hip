@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -155,6 +156,9 @@ struct shyft_hip_region {
         std::vector<double> key;
         dbuf<int32_t> idx, cnt;
         dbuf<double> w, aux;
+        dbuf<int32_t> wu, wn, ovf;  // wavefront unions of the neighbour lists (idw_wave_union)
+        dbuf<uint32_t> lidx;
+        bool wave_ok = false;
         int K = 0;
     } idw[N_FORCING];
     dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
@@ -913,6 +917,26 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
             nb.aux = tab.aux.p;
             nb.count = tab.cnt.p;
             hip_check(launch_idw_neighbours(nb, h->stream), "idw_neighbours");
+            // each wavefront's union of neighbour stations (the gather's compacted path when every union fits 64)
+            const size_t n_waves = (N + 63) / 64;
+            tab.wu.alloc(n_waves * 64);
+            tab.wn.alloc(n_waves);
+            tab.lidx.alloc(size_t((K + 3) / 4) * N);
+            tab.ovf.alloc(1);
+            hip_check(hipMemsetAsync(tab.ovf.p, 0, sizeof(int32_t), h->stream), "memset overflow");
+            idw_union_args ua;
+            ua.n_cells = int(N);
+            ua.max_members = K;
+            ua.idx = tab.idx.p;
+            ua.count = tab.cnt.p;
+            ua.wu = tab.wu.p;
+            ua.wn = tab.wn.p;
+            ua.lidx = tab.lidx.p;
+            ua.overflow = tab.ovf.p;
+            hip_check(launch_idw_wave_union(ua, h->stream), "idw_wave_union");
+            int32_t ovf = 1;
+            hip_check(region_copy(h, &ovf, tab.ovf.p, sizeof(int32_t), hipMemcpyDeviceToHost), "read overflow");
+            tab.wave_ok = ovf == 0;
             tab.key.swap(key);
         }
         idw_gather_args g;
@@ -933,6 +957,11 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
         g.count = tab.cnt.p;
         g.active = active;
         g.out = out;
+        // SHYFT_IDW_TILE=1: the row-tile gather even where the wavefront unions fit (tests cover both paths)
+        const bool wave = tab.wave_ok && !getenv("SHYFT_IDW_TILE");
+        g.wu = wave ? tab.wu.p : nullptr;
+        g.wn = wave ? tab.wn.p : nullptr;
+        g.lidx = wave ? tab.lidx.p : nullptr;
         hip_check(launch_idw_gather(g, h->stream), "idw_gather");
         hip_check(hipStreamSynchronize(h->stream), "idw");
     });

@@ -79,10 +79,14 @@ def test_c3_station_network_shape():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["wave", "tile"])
 @pytest.mark.parametrize("var,by_equation", [(0, False), (0, True), (1, False), (2, False), (3, False), (4, False)])
-def test_c3_idw_500_stations_730_rows_bitexact(var, by_equation):
-    """S = 500, 730 rows in one call plus a 2-call split (the neighbour table is reused): the multi-tile LDS
-    loop of the gather kernel against the oracle's run_interpolation (inverse_distance.h:142-250)."""
+def test_c3_idw_500_stations_730_rows_bitexact(var, by_equation, path, monkeypatch):
+    """S = 500, 730 rows in one call plus a 2-call split (the neighbour table is reused), against the oracle's
+    run_interpolation (inverse_distance.h:142-250): the wavefront-union gather (grid-ordered cells: every
+    wavefront's neighbours fit one 64-station list) and, with SHYFT_IDW_TILE=1, the multi-tile LDS loop."""
+    if path == "tile":
+        monkeypatch.setenv("SHYFT_IDW_TILE", "1")
     geo, xyz, vals = c3_region(1500, 730)
     kind = IDW_PARAMS[var][0]
     prm = list(C3_PARAMS[var])
@@ -132,10 +136,13 @@ def test_reference_4900_source_scenario_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["wave", "tile"])
 @pytest.mark.parametrize("with_nan", [False, True])
-def test_reference_4900_source_scenario_bitexact(with_nan):
-    """4900 sources: 3 x 4900 x 8 B of coordinates exceed the 32 KB LDS budget, so the gather reads rows from
-    global memory (lds_rows = 0), the path no other test reaches."""
+def test_reference_4900_source_scenario_bitexact(with_nan, path, monkeypatch):
+    """4900 sources: the wavefront-union gather, and (SHYFT_IDW_TILE=1) the tile kernel, where 3 x 4900 x 8 B of
+    coordinates exceed the 32 KB LDS budget, so the gather reads rows from global memory (lds_rows = 0)."""
+    if path == "tile":
+        monkeypatch.setenv("SHYFT_IDW_TILE", "1")
     from tests.test_idw import TEMPERATURE
     geo, xyz, vals, prm = reference_performance_scenario(72)
     if with_nan:
@@ -143,6 +150,21 @@ def test_reference_4900_source_scenario_bitexact(with_nan):
         vals = np.where(rng.uniform(size=vals.shape) < 0.1, np.nan, vals)
     exp = oracle_idw(TEMPERATURE, xyz, vals, geo[:, :3], prm)
     ok, msg = _same(_device_interpolate(geo, xyz, vals, 0, prm, [30]), exp)
+    assert ok, msg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("var", [0, 1])
+def test_c3_shuffled_cells_fall_back_to_tiles_bitexact(var):
+    """Cells in random order: a wavefront's 64 cells are scattered over the region, their neighbour lists need
+    more than 64 stations, so the union kernel reports the overflow and the gather keeps the row tiles."""
+    geo, xyz, vals = c3_region(1500, 100)
+    geo = geo[np.random.default_rng(5).permutation(geo.shape[0])]
+    kind = IDW_PARAMS[var][0]
+    prm = list(C3_PARAMS[var])
+    v = np.ascontiguousarray(vals[var])
+    exp = oracle_idw(kind, xyz, v, geo[:, :3], prm, dst_slope=geo[:, 5])
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, []), exp)
     assert ok, msg
 
 
