@@ -159,6 +159,9 @@ __device__ __noinline__ double gs_calc_q_general(double a, double b, double z, d
 
 __device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1, double a2, double b2, double q1,
                                                 double lga2) {
+#ifdef SHYFT_ABLATE_BRENT
+    return z1 * 0.5;  // instruction-budget ablation only (wrong results)
+#endif
     const double Q1 = q1 == q1 ? q1 : gs_calc_q_general(a1, b1, z1, dlgamma(a1));
     const gsb_k k = gsb_load();
     const double eps = detmath::gamma_snow_policy_eps(a2);

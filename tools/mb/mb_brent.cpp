@@ -83,6 +83,22 @@ __global__ __launch_bounds__(64) void calcq(const double* J, const double* lga2,
     if ((threadIdx.x & 63) == 0) cyc[g / 64] = t1 - t0;
 }
 
+// kirchner_step (dopri5, one hour) per lane, reps dependent calls: per-call instruction counts under rocprofv3 --pmc
+__global__ __launch_bounds__(64) void kirch(const double* x0, int reps, double* out, unsigned long long* cyc) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    double q = 0.5 + x0[g & 1023];
+    double acc = 0.0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < reps; ++r) {
+        double qa;
+        kirchner_step(q, qa, 0.4 + 0.01 * (r & 7), 0.05, 1.0, -2.439, 0.966, -0.10);
+        acc += qa;
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[g] = acc + q;
+    if ((threadIdx.x & 63) == 0) cyc[g / 64] = t1 - t0;
+}
+
 template <int K>
 __global__ __launch_bounds__(64) void chain(const double* x0, int reps, double* out, unsigned long long* cyc) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -168,6 +184,16 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(c.data(), cyc, waves * 8, hipMemcpyDeviceToHost));
         printf("calc_q        waves %5d: %7.0f cyc/eval (per wave), %.3g lane-evals/s\n", waves, mean_cyc(c) / creps,
                (double)waves * 64 * creps / (ms * 1e-3));
+    }
+    for (int waves : {1, 4096}) {
+        const int kreps = 20;
+        kirch<<<waves, 64>>>(x0, kreps, out, cyc);
+        CK(hipEventRecord(e0));
+        kirch<<<waves, 64>>>(x0, kreps, out, cyc);
+        CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+        std::vector<unsigned long long> c(waves);
+        CK(hipMemcpy(c.data(), cyc, waves * 8, hipMemcpyDeviceToHost));
+        printf("kirchner_step waves %5d: %7.0f cyc/call (per wave)\n", waves, mean_cyc(c) / kreps);
     }
     if (getenv("MB_QUICK")) { printf("MB_DONE\n"); return 0; }
     const char* names[] = {"dexp (call)", "exp (inline)", "fma", "div", "dlog (call)"};
