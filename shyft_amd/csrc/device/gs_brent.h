@@ -157,22 +157,95 @@ __device__ __noinline__ double gs_calc_q_general(double a, double b, double z, d
     return gs_calc_q(a, b, z, lga);
 }
 
-__device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1, double a2, double b2, double q1,
-                                                double lga2) {
-#ifdef SHYFT_ABLATE_BRENT
-    return z1 * 0.5;  // instruction-budget ablation only (wrong results)
-#endif
-    const double Q1 = q1 == q1 ? q1 : gs_calc_q_general(a1, b1, z1, dlgamma(a1));
-    const gsb_k k = gsb_load();
-    const double eps = detmath::gamma_snow_policy_eps(a2);
-    const double ap1 = a2 + 1.0;
-    const bool a_ok = a2 > 0.0;
-    auto f = [&](double z) {
+// f = (calc_q(a2, b2, z) - Q1)^2 of the job, fast path with the general fallback
+struct gsb_f {
+    double a2, b2, lga2, Q1, eps, ap1;
+    bool a_ok;
+    gsb_k k;
+    __device__ __forceinline__ gsb_f(double z1, double a1, double b1, double a2_, double b2_, double q1, double lga2_)
+        : a2(a2_), b2(b2_), lga2(lga2_) {
+        Q1 = q1 == q1 ? q1 : gs_calc_q_general(a1, b1, z1, dlgamma(a1));
+        k = gsb_load();
+        eps = detmath::gamma_snow_policy_eps(a2);
+        ap1 = a2 + 1.0;
+        a_ok = a2 > 0.0;
+    }
+    __device__ __forceinline__ double operator()(double z) const {
         bool ok;
         double cq = gsb_calc_q(a2, b2, z, lga2, eps, ap1, k, ok);
         if (!(ok && a_ok)) cq = gs_calc_q_general(a2, b2, z, lga2);  // the general path (rare)
         const double v = cq - Q1;
         return v * v;
+    }
+};
+
+// Speculative opening of the Brent search (small regions, where the solve is a latency problem). The first three
+// points boost's brent_find_minima evaluates do not depend on f's values: x = w = v = z1 opens; iteration 1 takes
+// the golden step u1 (delta2 starts at 0); iteration 2's parabola through (z1, u1) is degenerate whichever of
+// f(u1) <= f(z1) holds (r == q, so p = q = 0 and the golden step is taken again), so its point is u2a (x = u1,
+// max = z1) or u2b (x = z1, min = u1). gs_brent_point gives point k of {z1, u1, u2a, u2b} by the solver's own
+// formulas; four lanes evaluate f at the four points at once and the solver then looks each of its f arguments up
+// among them (bitwise) before evaluating. f is a pure function of its argument, so a hit returns the same bits;
+// where an assumption fails (non-finite f values, an early exit) the argument simply misses and is evaluated.
+__device__ __forceinline__ double gs_brent_point(double z1, int k) {
+    const double tolerance = 0x1p-11;
+    const double golden = (double)0.3819660f;
+    auto golden_step = [&](double x, double lo, double hi) {
+        const double mid = (lo + hi) / 2;
+        const double fract1 = tolerance * fabs(x) + tolerance / 4;
+        const double d2 = (x >= mid) ? lo - x : hi - x;
+        const double delta = golden * d2;
+        return (fabs(delta) >= fract1) ? (x + delta) : (delta > 0 ? x + fabs(fract1) : x - fabs(fract1));
+    };
+    if (k == 0) return z1;
+    const double u1 = golden_step(z1, 0.0, z1);
+    if (k == 1) return u1;
+    double lo = 0.0, hi = z1, x = z1;
+    if (k == 2) {  // f(u1) <= f(z1): x = u1, the old x bounds the side u1 moved from
+        if (u1 >= x) lo = x; else hi = x;
+        x = u1;
+    } else {  // f(u1) > f(z1): u1 bounds its side
+        if (u1 < x) lo = u1; else hi = u1;
+    }
+    return golden_step(x, lo, hi);
+}
+
+struct gsb_zf {
+    double z, f;
+};
+__device__ __noinline__ gsb_zf gs_corr_lwc_spec(double z1, double a1, double b1, double a2, double b2, double q1,
+                                                double lga2, int k) {
+    const gsb_f f(z1, a1, b1, a2, b2, q1, lga2);
+    gsb_zf r;
+    r.z = gs_brent_point(z1, k);
+    r.f = f(r.z);
+    return r;
+}
+
+struct gsb_memo {
+    double z[4], f[4];
+};
+
+template <bool MEMO>
+__device__ __forceinline__ double gs_corr_lwc_lean_t(double z1, double a1, double b1, double a2, double b2, double q1,
+                                                     double lga2, const gsb_memo* memo) {
+#ifdef SHYFT_ABLATE_BRENT
+    return z1 * 0.5;  // instruction-budget ablation only (wrong results)
+#endif
+    const gsb_f fe(z1, a1, b1, a2, b2, q1, lga2);
+    gsb_memo mm;
+    if (MEMO) mm = *memo;
+    auto f = [&](double z) {
+        if (MEMO) {
+            const long long zb = __double_as_longlong(z);
+            bool hit = false;
+            double r = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (!hit && zb == __double_as_longlong(mm.z[i])) { hit = true; r = mm.f[i]; }
+            if (hit) return r;
+        }
+        return fe(z);
     };
     double min = 0.0, max = z1;
     const double tolerance = 0x1p-11;  // ldexp(1, 1-12)
@@ -224,6 +297,16 @@ __device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1,
         }
     } while (--count);
     return x;
+}
+
+__device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1, double a2, double b2, double q1,
+                                                double lga2) {
+    return gs_corr_lwc_lean_t<false>(z1, a1, b1, a2, b2, q1, lga2, nullptr);
+}
+
+__device__ __noinline__ double gs_corr_lwc_memo(double z1, double a1, double b1, double a2, double b2, double q1,
+                                                double lga2, const gsb_memo& memo) {
+    return gs_corr_lwc_lean_t<true>(z1, a1, b1, a2, b2, q1, lga2, &memo);
 }
 
 }  // namespace shyft_dev

@@ -85,8 +85,9 @@ constexpr int BLOCK = SHYFT_BLOCK;
 // WAVES: the occupancy target. 4 waves per SIMD (128 VGPRs, spilling) is the measured best when the launch fills
 // the GPU; a region too small to give every SIMD 4 waves (<= 2 workgroups per CU, e.g. a strong-scaled shard of
 // 131K cells) gets the 2-wave instance instead (256 VGPRs, no spills): it cannot be 4-deep anyway.
-template <bool COMPACT, bool UNIFORM, bool ENS = false, int WAVES = SHYFT_LB_WAVES>
-__global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
+// B: cells (lanes) per workgroup. SPEC: the speculative Brent opening (device/gs_brent.h), for small regions.
+template <bool COMPACT, bool UNIFORM, bool ENS = false, int WAVES = SHYFT_LB_WAVES, int B = BLOCK, bool SPEC = false>
+__global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
     if (valid && a.active && !a.active[cell]) valid = false;
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
 #if SHYFT_PTGSK_LDSC
     // the cell constants live in LDS, not in VGPRs: each use reloads its lane's slot (the barriers of the
     // step keep the compiler from hoisting the loads), so none of them is live across the Brent phase
-    __shared__ double lcc[11][BLOCK];
+    __shared__ double lcc[11][B];
     {
         const int t = threadIdx.x;
         lcc[0][t] = gcell.forest_fraction;
@@ -180,7 +181,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
     const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
 
     // Brent job queue of the workgroup (COMPACT)
-    __shared__ double jz1[BLOCK], ja1[BLOCK], jb1[BLOCK], ja2[BLOCK], jb2[BLOCK], jq1[BLOCK], jlg2[BLOCK], jres[BLOCK];
+    __shared__ double jz1[B], ja1[B], jb1[B], ja2[B], jb2[B], jq1[B], jlg2[B], jres[B];
+    __shared__ double jsz[SPEC ? 64 : 1], jsf[SPEC ? 64 : 1];  // speculative opening: point and f of lane t
     __shared__ int jcount[2];
     if (COMPACT) {
         if (threadIdx.x == 0) jcount[0] = jcount[1] = 0;  // both: the first step may be odd (start_step)
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
 #ifdef SHYFT_PROF
                 const unsigned long long tb = __builtin_amdgcn_s_memtime();
                 int nf = 0;
-                for (int j = threadIdx.x; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j], nf);
+                for (int j = threadIdx.x; j < nj; j += B) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j], nf);
                 if (threadIdx.x < nj) {  // solver lanes: wave sum and wave max of f evaluations
                     int sum = nf, mx = nf;
                     for (int o = 32; o > 0; o >>= 1) {
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
 #else
 #ifdef SHYFT_ROTATE2
                 // the solving wavefront rotates with the step and the workgroup (SIMD load balance)
-                const int t = (threadIdx.x + BLOCK - 64 * ((i + (int)blockIdx.x) % (BLOCK / 64))) % BLOCK;
+                const int t = (threadIdx.x + B - 64 * ((i + (int)blockIdx.x) % (B / 64))) % B;
 #else
                 const int t = threadIdx.x;
 #endif
@@ -275,7 +277,30 @@ __global__ __launch_bounds__(BLOCK, WAVES) void ptgsk_run_kernel(const ptgsk_kar
                 // barrier below): it gets issue priority over the other workgroups' wavefronts on its SIMD
                 if (t < nj) __builtin_amdgcn_s_setprio(SHYFT_BRENT_PRIO);
 #endif
-                for (int j = t; j < nj; j += BLOCK) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
+                // the speculative opening when the jobs' point lanes fit the solving wavefront: 4 lanes per job
+                // (z1, u1, u2a, u2b: two f rounds saved) or 2 (z1, u1: one round saved)
+                const int L = SPEC ? (4 * nj <= 64 ? 4 : 2 * nj <= 64 ? 2 : 0) : 0;
+                if (L) {
+                    const int jj = L == 4 ? t >> 2 : t >> 1;
+                    if (t < 64 && jj < nj) {
+                        const gsb_zf r = gs_corr_lwc_spec(jz1[jj], ja1[jj], jb1[jj], ja2[jj], jb2[jj], jq1[jj], jlg2[jj], t & (L - 1));
+                        jsz[t] = r.z;
+                        jsf[t] = r.f;
+                    }
+                    __syncthreads();
+                    if (t < nj) {
+                        gsb_memo mm;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {  // with 2 points, entries 2 and 3 repeat entry 0
+                            const int e = L * t + (k < L ? k : 0);
+                            mm.z[k] = jsz[e];
+                            mm.f[k] = jsf[e];
+                        }
+                        jres[t] = gs_corr_lwc_memo(jz1[t], ja1[t], jb1[t], ja2[t], jb2[t], jq1[t], jlg2[t], mm);
+                    }
+                } else {
+                    for (int j = t; j < nj; j += B) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
+                }
 #if SHYFT_BRENT_PRIO > 0
                 __builtin_amdgcn_s_setprio(0);
 #endif
@@ -637,15 +662,30 @@ hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t
     const bool small = force ? force[0] == '2' : grid <= 2 * n_cu;
     if (a.fcol)
         hipLaunchKernelGGL((ptgsk_run_kernel<true, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (SHYFT_COMPACT_DEFAULT)
-        if (a.uniform_params) {
-            if (small) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            else hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (SHYFT_COMPACT_DEFAULT && small) {
+        // small regions: one-wavefront workgroups (each wavefront solves its own ~7 winter Brent jobs: no workgroup
+        // barrier wait) with the speculative Brent opening (4 lanes per job, free in a wavefront that has the lanes)
+        static const char* sm = getenv("SHYFT_PTGSK_SMALL");  // measurement knob: "256" = the 256-lane instance,
+        const int smode = sm ? atoi(sm) : 64;                 // "65" = 64 lanes without the speculation
+        const int g64 = (a.n_cells + 63) / 64;
+        if (smode == 256) {
+            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
+            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        } else if (smode == 65) {
+            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2, 64, false>), dim3(g64), dim3(64), 0, stream, a);
+            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2, 64, false>), dim3(g64), dim3(64), 0, stream, a);
         } else {
-            if (small) hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
+            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
         }
-    else
+    } else if (SHYFT_COMPACT_DEFAULT) {
+        static const char* sp = getenv("SHYFT_PTGSK_SPEC");  // measurement knob: "1" = speculative opening
+        if (sp && sp[0] == '1') {
+            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, SHYFT_LB_WAVES, BLOCK, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, SHYFT_LB_WAVES, BLOCK, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        } else if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    } else
         hipLaunchKernelGGL((ptgsk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

@@ -64,19 +64,21 @@ def main():
         elif k == "--stack":
             stack = v
     ref = None
-    for lib in args:
+    for spec in args:  # lib.so[:VAR=value[:VAR=value...]] -- environment settings for that run
+        lib, *envs = spec.split(":")
         env = dict(os.environ, SHYFT_HIP_LIB=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in envs)
         out = subprocess.run([sys.executable, "-c", CODE, str(cells), str(chunks), stack], env=env, capture_output=True,
                              text=True, timeout=600)
         try:
             d = json.loads(out.stdout.strip().splitlines()[-1])
         except Exception:
-            print(os.path.basename(lib), "FAILED", out.stderr[-1500:], flush=True)
+            print(spec, "FAILED", out.stderr[-1500:], flush=True)
             continue
         if ref is None:
             ref = d["digest"]
         ms = d["ms"]
-        print(f"{os.path.basename(lib):28s} mean {sum(ms) / len(ms):7.1f} ms  "
+        print(f"{os.path.basename(spec):28s} mean {sum(ms) / len(ms):7.1f} ms  "
               f"{'bit-exact' if d['digest'] == ref else 'DIFFERS ' + d['digest']}  "
               + " ".join(f"{m:.0f}" for m in ms), flush=True)
 
