@@ -679,11 +679,9 @@ hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t
             else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
         }
     } else if (SHYFT_COMPACT_DEFAULT) {
-        static const char* sp = getenv("SHYFT_PTGSK_SPEC");  // measurement knob: "1" = speculative opening
-        if (sp && sp[0] == '1') {
-            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, SHYFT_LB_WAVES, BLOCK, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, SHYFT_LB_WAVES, BLOCK, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        } else if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        // (the speculative Brent opening in this instance measured 100.5 -> 134.7 ms per 1M-cell chunk, year mean:
+        // its memo registers spill in every phase of the 128-VGPR step loop, so it stays a small-region feature)
+        if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
         else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     } else
         hipLaunchKernelGGL((ptgsk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);

@@ -1,0 +1,68 @@
+"""Every pt_gs_k kernel instance the launcher can pick, bit for bit against the oracle on the same region.
+
+launch_ptgsk_run (kernels/ptgsk.hip) picks the instance by region size: regions of at most two 256-lane
+workgroups per CU run 64-lane workgroups with the speculative Brent opening (device/gs_brent.h), larger ones the
+256-lane 4-wave instance. The other parity tests run small regions, so they cover the first; this test forces the
+others on a small region through the launcher's measurement knobs (read once per process, hence a child process
+per instance). The region is C1's 200 cells over January-April (snowfall, corr_lwc Brent jobs, melt), with all
+8 response series, the state series and the final state compared.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from shyft_amd import synthetic
+from tests import engines
+
+pytestmark = pytest.mark.gpu
+
+N, T = 200, 2880
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from shyft_amd import synthetic
+from tests import engines
+n, T = int(sys.argv[2]), int(sys.argv[3])
+geo = synthetic.geo11(n)
+f = synthetic.forcing(n, 0, T, synthetic.SEED)
+params = synthetic.default_ptgsk_parameters()
+state = synthetic.default_ptgsk_state(n)
+g = engines.run("hip", geo, params, state, synthetic.T0_2015_US, synthetic.HOUR_US, f, full=True, collect_state=True)
+np.savez(sys.argv[4], full=np.asarray(g["full"]), ss=np.asarray(g["state_series"]), st=np.asarray(g["state"]))
+'''
+
+
+@pytest.fixture(scope="module")
+def oracle_run():
+    geo = synthetic.geo11(N)
+    f = synthetic.forcing(N, 0, T, synthetic.SEED)
+    params = synthetic.default_ptgsk_parameters()
+    state = synthetic.default_ptgsk_state(N)
+    c = engines.run("oracle", geo, params, state, synthetic.T0_2015_US, synthetic.HOUR_US, f, full=True,
+                    collect_state=True)
+    return np.asarray(c["full"]), np.asarray(c["state_series"]), np.asarray(c["state"])
+
+
+@pytest.mark.parametrize("env", [
+    {"SHYFT_PTGSK_WAVES": "4"},                           # 256 lanes, 4 waves per SIMD (regions > 131K cells)
+    {"SHYFT_PTGSK_SMALL": "256"},                          # 256 lanes, 2 waves per SIMD
+    {"SHYFT_PTGSK_SMALL": "65"},                           # 64 lanes without the speculative opening
+    {},                                                    # the default small-region instance
+], ids=["w4", "w2-256", "w2-64", "default"])
+def test_instance_bitexact(env, oracle_run, tmp_path):
+    out = tmp_path / "g.npz"
+    e = dict(os.environ, **env)
+    r = subprocess.run([sys.executable, "-c", CHILD, ROOT, str(N), str(T), str(out)], env=e, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    g = np.load(out)
+    full, ss, st = oracle_run
+    for name, a, b in (("response series", g["full"], full), ("state series", g["ss"], ss), ("final state", g["st"], st)):
+        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        assert same.all(), f"{json.dumps(env)} {name}: {int((~same).sum())} values differ"
