@@ -9,6 +9,7 @@
 // discharge/charge out per cell.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../device/hbv_dev.h"
 #include "../device/pt_dev.h"
@@ -63,15 +64,19 @@ constexpr int BLOCK = 256;
 #define HBV_ST(p, v) ((p) = (v))
 #endif
 
-template <bool UNIFORM, int NB>
+// LEAN: the instance for the common launch (discharge collector only, no state series, no ensemble forcing columns):
+// those paths and their
+// pointers are compiled out, which keeps the step loop's scalar registers (the uniform parameter row, the series
+// bases) within the SGPR file instead of spilled to VGPR lanes (a v_readlane_b32, VALU issue, per use)
+template <bool UNIFORM, int NB, bool LEAN = false>
 __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;
     const size_t N = (size_t)a.n_cells;
     // forcing column: the lane itself, or the shared cell of a parameter-ensemble lane
-    const size_t NF = a.fcol ? (size_t)a.f_cols : N;
-    const size_t fcl = a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
+    const size_t NF = !LEAN && a.fcol ? (size_t)a.f_cols : N;
+    const size_t fcl = !LEAN && a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
     const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * HBV_NP;
 #if SHYFT_HBV_PRELOAD
     // the uniform parameter row is read again in every step (scalar loads, constant-cache hits) instead of held
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * NF;
     double* __restrict__ R = a.resp;
     const size_t RS = TW * N;
-    double* __restrict__ SS = a.state_series;
+    double* __restrict__ SS = LEAN ? nullptr : a.state_series;
     const size_t SSS = (TW + 1) * N;
 
     auto collect_state = [&](size_t wi) {  // state_collector::collect (hbv_stack_cell_model.h:196-212)
@@ -254,13 +259,13 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
         HBV_ST(R[HR_AVG_DISCHARGE * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
         HBV_ST(R[HR_CHARGE_M3S * RS + fo], charge_m3s);
-        if (a.collect >= 1) {
+        if (!LEAN && a.collect >= 1) {
             // response.snow.snow_state is never written by hbv_snow::step (hbv_snow.h:121-124): the
             // reference collects its default (swe = sca = 0)
             R[HR_SNOW_SCA * RS + fo] = 0.0;
             R[HR_SNOW_SWE * RS + fo] = 0.0;
         }
-        if (a.collect >= 2) {
+        if (!LEAN && a.collect >= 2) {
             R[HR_SNOW_OUTFLOW * RS + fo] = cell_area_m2 * snow_outflow * mmh_to_m3s_scale_factor;
             R[HR_GLACIER_MELT * RS + fo] = gm_melt_m3s;
             R[HR_AE_OUTPUT * RS + fo] = ae;
@@ -291,7 +296,11 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
+    static const char* lean_env = getenv("SHYFT_HBV_LEAN");  // measurement knob: "0" = the general 5-bin instance
+    const bool lean = !lean_env || lean_env[0] != '0';
+    if (a.uniform_params && a.nb_max <= 5 && !a.state_series && !a.fcol && a.collect == 0 && lean)
+        hipLaunchKernelGGL((hbv_run_kernel<true, 5, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
         hipLaunchKernelGGL((hbv_run_kernel<true, 5>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.uniform_params)
         hipLaunchKernelGGL((hbv_run_kernel<true, HBV_MAX_BINS>), dim3(grid), dim3(BLOCK), 0, stream, a);

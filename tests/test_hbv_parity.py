@@ -62,6 +62,9 @@ def test_hbv_synthetic_winter_to_melt_bitexact():
     got = engines.run_hbv("hip", geo, p, st, synthetic.T0_2015_US, HOUR, f, collect_state=True)
     assert np.nanmax(ref["state_series"][0]) > 10.0  # snow did accumulate
     _assert_same(got, ref, ["full", "state", "state_series"])
+    # the discharge collector alone (no state series, one 5-bin parameter set): the LEAN kernel instance
+    lean = engines.run_hbv("hip", geo, p, st, synthetic.T0_2015_US, HOUR, f, full=False)
+    _assert_same(lean, ref, ["main", "state"])
 
 
 @pytest.mark.gpu
