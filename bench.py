@@ -3,10 +3,11 @@
 
 Workload (BASELINE.json configs[1]): pt_gs_k, 1M synthetic cells per GPU x 8760
 hourly steps, fp64. A bench "step" is one pass of the hot path over one batch:
-all cells of the rank advanced through one chunk of CHUNK=730 hourly steps
-(1/12 year) -- the chunk's forcing is generated into HBM by the device
+all cells of the rank advanced through one chunk of CHUNK=438 hourly steps
+(1/20 year) -- the chunk's forcing is generated into HBM by the device
 generator and run_cells runs the pt_gs_k kernel over it, state
-carried in HBM to the next chunk. --steps 12 therefore runs one full year.
+carried in HBM to the next chunk. --steps 20 (the default, and the driver's
+command) therefore runs exactly configs[1]'s year: Jan 1 - Dec 31, 8760 steps.
 The per-cell fp64 forcing of a full year (350 GB at 1M cells) does not fit
 one GPU's 288 GB, hence the chunking; generating a chunk costs ~1% of the step
 and is inside the timed region (conservative).
@@ -41,7 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "cell-steps/sec (cells×timesteps/wall) for pt_gs_k at 1/2/4/8 MI355X"
-CHUNK = 730
+CHUNK = 438                      # 20 chunks = one calendar year (8760 hourly steps)
 YEAR = 8760
 HBM_PEAK_BPS = 8.0e12            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic HBM bytes of the dominant kernel
@@ -59,7 +60,7 @@ STACKS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=YEAR // CHUNK)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=0,
                     help="cells per GPU (default 1,048,576 for pt_gs_k, 524,288 for hbv_stack)")
@@ -496,7 +497,7 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
 
 
 def workload_tag(a, cells):

@@ -137,6 +137,12 @@ int shyft_hip_get_forcing(const shyft_hip_region* h, int var, size_t step0, size
  * built on the first call and reused while sources and parameters are unchanged. */
 int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const double* src_xyz,
                           const double* src_values, size_t step0, size_t n, const double* idw_param);
+/* Which gather the last shyft_hip_interpolate of variable var ran (no reference counterpart: a test and
+ * measurement aid): SHYFT_HIP_IDW_WAVE (every wavefront's neighbour union fits 64 stations: the compacted
+ * wavefront-union gather), SHYFT_HIP_IDW_TILE (the row-tile gather), SHYFT_HIP_IDW_COPY (one temperature source
+ * copied), SHYFT_HIP_IDW_NONE (no interpolation of var yet). Returns -1 on a bad handle or variable. */
+enum shyft_hip_idw_path { SHYFT_HIP_IDW_NONE = 0, SHYFT_HIP_IDW_TILE = 1, SHYFT_HIP_IDW_WAVE = 2, SHYFT_HIP_IDW_COPY = 3 };
+int shyft_hip_interpolation_path(const shyft_hip_region* h, int var);
 
 /* Bayesian temperature kriging of the temperature forcing into the calculated cells, steps [step0, step0+n)
  * of the resident window: region_model::interpolate's default temperature method
@@ -174,7 +180,9 @@ int shyft_hip_synchronize(shyft_hip_region* h);
 /* Double-buffered forcing window (measurement / pipelining aid, no reference counterpart): generate the synthetic
    forcing of the window starting at w0_next into a second buffer on a side stream restricted to n_cus CUs (<= 0:
    no restriction) while the current window runs; shyft_hip_swap_forcing_window(h, w0_next) then makes it the
-   region's window (the next run waits for the generator on the device). */
+   region's window (the next run waits for the generator on the device). The swap does not NaN-fill the response
+   and state-series rows: a run over the new window must follow before they are read. A pending prefetch is
+   dropped when the time axis or window length changes (shyft_hip_set_time_axis). */
 int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t w0_next,
                                          int n_cus);
 int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next);

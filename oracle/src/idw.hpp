@@ -113,11 +113,13 @@ inline std::vector<neighbour> neighbours(const geo_point& d, const std::vector<s
     return swl;
 }
 
-// run_interpolation (inverse_distance.h:142-250) for one model over [0, T)
+// run_interpolation (inverse_distance.h:142-250) for one model over [0, T), destinations [j0, j1) (default all;
+// the destinations are independent, so the caller may split them over threads)
 inline void run(model_kind kind, const std::vector<source>& src, const std::vector<destination>& dst, size_t T,
-                const parameter& p, double* out /*[T][n_dst]*/) {
+                const parameter& p, double* out /*[T][n_dst]*/, size_t j0 = 0, size_t j1 = SIZE_MAX) {
     const size_t N = dst.size();
-    for (size_t j = 0; j < N; ++j) {
+    if (j1 > N) j1 = N;
+    for (size_t j = j0; j < j1; ++j) {
         const auto nb = neighbours(dst[j].p, src, p);
         std::vector<geo_point> pts;
         std::vector<double> tv;

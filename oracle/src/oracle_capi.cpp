@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstring>
 #include <exception>
+#include <thread>
 
 #include "common.hpp"
 #include "idw.hpp"
@@ -250,7 +251,16 @@ extern "C" int oracle_idw_run(int kind, size_t S, const double* src_xyz, const d
     std::vector<idw::destination> dst(N);
     for (size_t j = 0; j < N; ++j)
         dst[j] = idw::destination{geo_point(dst_xyz[3 * j], dst_xyz[3 * j + 1], dst_xyz[3 * j + 2]), dst_slope ? dst_slope[j] : 0.9};
-    idw::run(idw::model_kind(kind), src, dst, T, p, out);
+    // destinations are independent: split over up to 16 threads (each writes its own columns of out)
+    const size_t n_thr = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), (N + 255) / 256});
+    if (n_thr <= 1) {
+        idw::run(idw::model_kind(kind), src, dst, T, p, out);
+        return 0;
+    }
+    std::vector<std::thread> pool;
+    for (size_t k = 0; k < n_thr; ++k)
+        pool.emplace_back([&, k] { idw::run(idw::model_kind(kind), src, dst, T, p, out, N * k / n_thr, N * (k + 1) / n_thr); });
+    for (auto& t : pool) t.join();
     return 0;
 }
 

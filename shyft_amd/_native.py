@@ -40,6 +40,7 @@ SIGNATURES = {
     "shyft_hip_synthetic_forcing": (C.c_int, [_h, C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t]),
     "shyft_hip_interpolate": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
                                         C.c_void_p]),
+    "shyft_hip_interpolation_path": (C.c_int, [_h, C.c_int]),
     "shyft_hip_interpolate_btk": (C.c_int, [_h, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
                                             C.c_void_p, C.c_void_p]),
     "shyft_hip_btk": (C.c_int, [C.c_int, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,

@@ -160,6 +160,7 @@ struct shyft_hip_region {
         dbuf<uint32_t> lidx;
         bool wave_ok = false;
         int K = 0;
+        int last_path = SHYFT_HIP_IDW_NONE;  // the gather the last interpolate of this variable ran
     } idw[N_FORCING];
     dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
     bool dst_dirty = true;
@@ -383,8 +384,16 @@ void update_derived(shyft_hip_region* h) {
     h->derived_dirty = false;
 }
 
+// a pending shyft_hip_prefetch_synthetic_forcing is dropped: its buffer has the old window's shape
+void cancel_prefetch(shyft_hip_region* h) {
+    if (h->gen_stream) hip_check(hipStreamSynchronize(h->gen_stream), "sync generator");
+    h->gen_w0 = SIZE_MAX;
+    h->d_forcing_next.release();
+}
+
 void alloc_window(shyft_hip_region* h) {
     const size_t N = h->n;
+    cancel_prefetch(h);
     h->d_forcing.alloc(N_FORCING * h->TW * N);
     hip_check(launch_fill(h->d_forcing.p, h->d_forcing.n, NAN, h->stream), "fill forcing");
     h->d_resp.alloc(h->n_series() * h->TW * N);
@@ -513,6 +522,7 @@ void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (h->ens) shyft_hip_region_destroy(h->ens);
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->gen_stream) (void)hipStreamSynchronize(h->gen_stream);  // a prefetch may still write d_forcing_next
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->ev_mid) (void)hipEventDestroy(h->ev_mid);
@@ -827,7 +837,7 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
         // the buffer was last read by a run on the region stream: the generator waits for that stream first
         hip_check(hipEventRecord(h->ev_gen, h->stream), "record");
         hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_gen, 0), "wait");
-        const int blocks = 16 * (n_cus > 0 ? n_cus : 256);  // 4 workgroups of 4 waves per CU
+        const int blocks = 4 * (n_cus > 0 ? n_cus : 256);  // 4 workgroups of 4 waves per CU (grid-stride over cells)
         hip_check(launch_synthetic_forcing_stream(h->d_forcing_next.p, h->TW, 0, h->TW, h->n, seed, cell_offset,
                                                   w0_next, h->d_alt.p, blocks, h->gen_stream),
                   "synthetic_forcing (prefetch)");
@@ -840,6 +850,11 @@ int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next) {
     if (!h) return fail(h, "shyft_hip_swap_forcing_window: null handle");
     return guarded(h, [&] {
         if (h->gen_w0 != w0_next) throw std::runtime_error("swap_forcing_window: no prefetched window at this step");
+        if (h->d_forcing_next.n != h->d_forcing.n || w0_next + h->TW > h->T)
+            throw std::runtime_error("swap_forcing_window: the prefetched window does not match the region's window");
+        // the response / state-series rows still hold the previous window's values (no NaN fill, unlike
+        // set_window): the run that follows the swap rewrites them, and reading them before it is the caller's
+        // error (shyft_hip.h)
         // later work on the region stream (the next run) waits for the generator, without a host wait
         hip_check(hipStreamWaitEvent(h->stream, h->ev_gen, 0), "wait generator");
         std::swap(h->d_forcing.p, h->d_forcing_next.p);
@@ -868,6 +883,7 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
             // one temperature source: copied to the cells (region_model.h:470-481)
             hip_check(launch_copy_source(h->d_src_vals.p, int(n), int(N), active, out, h->stream), "copy_source");
             hip_check(hipStreamSynchronize(h->stream), "sync");
+            h->idw[var].last_path = SHYFT_HIP_IDW_COPY;
             return;
         }
         static const int kind_of_var[N_FORCING] = {IDW_TEMPERATURE, IDW_PRECIPITATION, IDW_WIND_SPEED, IDW_REL_HUM,
@@ -964,7 +980,13 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
         g.lidx = wave ? tab.lidx.p : nullptr;
         hip_check(launch_idw_gather(g, h->stream), "idw_gather");
         hip_check(hipStreamSynchronize(h->stream), "idw");
+        tab.last_path = wave ? SHYFT_HIP_IDW_WAVE : SHYFT_HIP_IDW_TILE;
     });
+}
+
+int shyft_hip_interpolation_path(const shyft_hip_region* h, int var) {
+    if (!h || var < 0 || var >= N_FORCING) return -1;
+    return h->idw[var].last_path;
 }
 
 namespace {
@@ -1260,10 +1282,11 @@ static void finish_run(shyft_hip_region* h) {
 // argument checks of region_model::run_cells (region_model.h:579-592), shared by the synchronous and the
 // asynchronous entry
 static void check_run_args(const shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {
-    // the reference's ncore is the host's hardware_concurrency (region_model.h:280); 0 -> its minimum 4
-    size_t ncore = std::thread::hardware_concurrency();
-    if (ncore == 0) ncore = 4;
-    if (use_ncore > 100 * ncore)
+    // the reference's ncore is the host's hardware_concurrency (region_model.h:280); its "reasonable minimum" of 4
+    // is substituted only on the use_ncore == 0 branch (region_model.h:579-584), so with ncore == 0 any
+    // use_ncore > 0 is rejected, as there
+    const size_t ncore = std::thread::hardware_concurrency();
+    if (use_ncore != 0 && use_ncore > 100 * ncore)
         throw std::runtime_error("illegal parameter value: use_ncore(" + std::to_string(use_ncore) +
                                  " is more than 100 time available physical cores: " + std::to_string(ncore));
     if (!(h->T > 0)) throw std::runtime_error("region_model::run with invalid time_axis invoked");

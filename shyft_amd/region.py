@@ -145,6 +145,13 @@ class HipRegion:
         self._chk(self._L.shyft_hip_interpolate(self.h, var, xyz.shape[0], _ptr(xyz), _ptr(v), step0, v.shape[0],
                                                 _ptr(p)))
 
+    def interpolation_path(self, var: int) -> str:
+        """The gather the last interpolate of `var` ran: "wave", "tile", "copy" or "none"."""
+        k = int(self._L.shyft_hip_interpolation_path(self.h, int(var)))
+        if k < 0:
+            raise ValueError(f"interpolation_path: invalid variable {var}")
+        return ("none", "tile", "wave", "copy")[k]
+
     def interpolate_btk(self, src_xyz: np.ndarray, src_values: np.ndarray, step0: int, btk_param,
                         prior_gradient=None):
         """Bayesian temperature kriging into the temperature forcing (src_values [n][S] on the model axis).

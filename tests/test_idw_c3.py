@@ -1,11 +1,16 @@
 """BASELINE configs[2] (C3) parity: inverse-distance interpolation from S = 500 stations, and the chained
 IDW -> pt_gs_k run, device against the oracle, bit for bit.
 
-The gather kernel stages station rows through LDS a tile at a time; at 500 stations the temperature tile holds
-5 rows (32 KB budget minus the station coordinates), so a 730-row chunk runs ~146 tiles with their barriers and
-per-tile finite-row flags. Above ~1365 sources a row set no longer fits and the kernel reads rows from global
-memory (lds_rows = 0); the reference's own 70 x 70 = 4900-source scenario
-(test/inverse_distance_test.cpp:396-450, "test_performance") covers that path.
+Two gather kernels exist and every test asserts which one ran (shyft_hip_interpolation_path):
+- the wavefront-union gather, taken when every wavefront's 64 cells draw their neighbours from at most 64
+  stations. On the C3 station grid (45 km spacing scaled to the region) that holds from ~65K grid-ordered cells
+  up (the bench's 1M-cell region: unions of 26-30), not at 1500 cells, where a wavefront spans 1.7 grid rows of a
+  39 km wide region and its union covers most of the 500 stations;
+- the row-tile gather (SHYFT_IDW_TILE=1 forces it; a region whose unions overflow falls back to it). At 500
+  stations the temperature tile holds 5 rows (32 KB budget minus the station coordinates), so a 730-row chunk runs
+  ~146 tiles with their barriers and per-tile finite-row flags. Above ~1365 sources a row set no longer fits and
+  the kernel reads rows from global memory (lds_rows = 0); the reference's own 70 x 70 = 4900-source scenario
+  (test/inverse_distance_test.cpp:396-450, "test_performance") covers that path.
 """
 import math
 import os
@@ -38,7 +43,9 @@ def c3_region(n_cells, rows, step0=0, nan_frac=0.03, seed=11):
     return geo, xyz, vals
 
 
-def _device_interpolate(geo, xyz, vals, var, prm, splits):
+def _device_interpolate(geo, xyz, vals, var, prm, splits, path=None):
+    """Interpolate var over the rows of vals in the calls [0, s1), [s1, s2), ... on a fresh region; `path`, if
+    given, is the gather every call must have run ("wave" / "tile")."""
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K
     T, N = vals.shape[0], geo.shape[0]
@@ -47,9 +54,12 @@ def _device_interpolate(geo, xyz, vals, var, prm, splits):
         r.set_geo(geo)
         r.set_parameters(synthetic.default_ptgsk_parameters())
         r.set_time_axis(synthetic.T0_2015_US, HOUR, T)
+        assert r.interpolation_path(var) == "none"
         b = 0
         for e in list(splits) + [T]:
             r.interpolate(var, xyz, vals[b:e], b, prm)
+            if path is not None:
+                assert r.interpolation_path(var) == path, f"rows [{b},{e}): ran {r.interpolation_path(var)}"
             b = e
         return r.get_forcing(var, 0, T)
     finally:
@@ -78,25 +88,75 @@ def test_c3_station_network_shape():
     assert np.isnan(vals).any() and np.isfinite(vals).mean() > 0.99
 
 
+def _wave_unions(geo, xyz, K, max_distance=200000.0):
+    """numpy restatement of the neighbour selection (distance order; the C3 case has no weight ties that could
+    reorder members) -> the size of each 64-cell wavefront's station union."""
+    d2 = ((geo[:, None, 0] - xyz[None, :, 0]) ** 2 + (geo[:, None, 1] - xyz[None, :, 1]) ** 2 +
+          (geo[:, None, 2] - xyz[None, :, 2]) ** 2)
+    d2 = np.where(d2 <= max_distance ** 2, d2, np.inf)
+    nb = np.argsort(d2, axis=1, kind="stable")[:, :K]
+    return [np.unique(nb[b:b + 64]).size for b in range(0, geo.shape[0], 64)]
+
+
+# C3 parity regions: 1500 cells (every wavefront union overflows 64 stations -> row tiles) and 65,536 cells (the
+# largest union is ~52 -> the wavefront-union gather), both with the bench's station grid scaled to the region
+C3_TILE_CELLS, C3_WAVE_CELLS = 1500, 1 << 16
+C3_ROWS = 730
+
+
+def test_c3_wave_union_geometry():
+    """The two test regions are on the intended side of the 64-station limit (checked on the host, the same
+    neighbour rule as the kernels): at 65,536 grid-ordered cells every union of K = 20 fits, at 1500 cells
+    none does -- so the device assertions on the path below test what they claim to test."""
+    g, x, _ = c3_region(C3_WAVE_CELLS, 1)
+    sel = np.arange(0, C3_WAVE_CELLS, 97 * 64)          # every 97th wavefront (the full 65K x 500 distance
+    rows = np.concatenate([np.arange(b, b + 64) for b in sel])   # matrix is 0.26 GB)
+    assert max(_wave_unions(g[rows], x, 20)) <= 64
+    g, x, _ = c3_region(C3_TILE_CELLS, 1)
+    assert min(_wave_unions(g, x, 20)) > 64
+
+
+_ORACLE_CACHE = {}
+
+
+def _c3_case(n_cells, var, by_equation):
+    key = (n_cells, var, by_equation)
+    if key not in _ORACLE_CACHE:
+        geo, xyz, vals = c3_region(n_cells, C3_ROWS)
+        prm = list(C3_PARAMS[var])
+        prm[5] = 1.0 if by_equation else 0.0
+        v = np.ascontiguousarray(vals[var])
+        exp = oracle_idw(IDW_PARAMS[var][0], xyz, v, geo[:, :3], prm, dst_slope=geo[:, 5])
+        assert np.isfinite(exp).all()   # 500 stations within 200 km: every cell always has a valid neighbour
+        _ORACLE_CACHE.clear()           # one region at a time (65K x 730 doubles per entry)
+        _ORACLE_CACHE[key] = (geo, xyz, v, prm, exp)
+    return _ORACLE_CACHE[key]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wave", "tile"])
 @pytest.mark.parametrize("var,by_equation", [(0, False), (0, True), (1, False), (2, False), (3, False), (4, False)])
 def test_c3_idw_500_stations_730_rows_bitexact(var, by_equation, path, monkeypatch):
     """S = 500, 730 rows in one call plus a 2-call split (the neighbour table is reused), against the oracle's
-    run_interpolation (inverse_distance.h:142-250): the wavefront-union gather (grid-ordered cells: every
-    wavefront's neighbours fit one 64-station list) and, with SHYFT_IDW_TILE=1, the multi-tile LDS loop."""
+    run_interpolation (inverse_distance.h:142-250), on the 65,536-cell C3 region: the wavefront-union gather
+    (asserted: every wavefront's neighbours fit one 64-station list) and, with SHYFT_IDW_TILE=1, the multi-tile
+    LDS loop (asserted) over the same cells."""
     if path == "tile":
         monkeypatch.setenv("SHYFT_IDW_TILE", "1")
-    geo, xyz, vals = c3_region(1500, 730)
-    kind = IDW_PARAMS[var][0]
-    prm = list(C3_PARAMS[var])
-    prm[5] = 1.0 if by_equation else 0.0
-    v = np.ascontiguousarray(vals[var])
-    exp = oracle_idw(kind, xyz, v, geo[:, :3], prm, dst_slope=geo[:, 5])
-    assert np.isfinite(exp).all()   # 500 stations within 200 km: every cell always has a valid neighbour
-    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, []), exp)
+    geo, xyz, v, prm, exp = _c3_case(C3_WAVE_CELLS, var, by_equation)
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, [], path=path), exp)
     assert ok, msg
-    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, [333]), exp)
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, [333], path=path), exp)
+    assert ok, msg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("var,by_equation", [(0, False), (0, True), (1, False), (4, False)])
+def test_c3_small_region_overflowing_unions_take_tiles_bitexact(var, by_equation):
+    """1500 cells: every wavefront union exceeds 64 stations, so the launch falls back to the row tiles without
+    being told to (asserted), and is bit-exact there too."""
+    geo, xyz, v, prm, exp = _c3_case(C3_TILE_CELLS, var, by_equation)
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, [333], path="tile"), exp)
     assert ok, msg
 
 
@@ -149,7 +209,7 @@ def test_reference_4900_source_scenario_bitexact(with_nan, path, monkeypatch):
         rng = np.random.default_rng(3)
         vals = np.where(rng.uniform(size=vals.shape) < 0.1, np.nan, vals)
     exp = oracle_idw(TEMPERATURE, xyz, vals, geo[:, :3], prm)
-    ok, msg = _same(_device_interpolate(geo, xyz, vals, 0, prm, [30]), exp)
+    ok, msg = _same(_device_interpolate(geo, xyz, vals, 0, prm, [30], path=path), exp)
     assert ok, msg
 
 
@@ -164,7 +224,7 @@ def test_c3_shuffled_cells_fall_back_to_tiles_bitexact(var):
     prm = list(C3_PARAMS[var])
     v = np.ascontiguousarray(vals[var])
     exp = oracle_idw(kind, xyz, v, geo[:, :3], prm, dst_slope=geo[:, 5])
-    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, []), exp)
+    ok, msg = _same(_device_interpolate(geo, xyz, v, var, prm, [], path="tile"), exp)
     assert ok, msg
 
 
@@ -172,20 +232,19 @@ def test_c3_shuffled_cells_fall_back_to_tiles_bitexact(var):
 def test_c3_chain_idw_then_pt_gs_k_bitexact():
     """run_interpolation (all five variables by IDW from the 500 stations, use_idw_for_temperature) followed by
     run_cells, against the same chain on the oracle: region_model::interpolate (region_model.h:397-555) feeding
-    cell::run (pt_gs_k_cell_model.h:243-262)."""
+    cell::run (pt_gs_k_cell_model.h:243-262). 65,536 cells, so every variable takes the wavefront-union gather
+    (asserted); the interpolated forcing is compared for every cell, the pt_gs_k run on 1024 sampled cells (the
+    oracle run on just those cells, from the oracle's own interpolated forcing)."""
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_ALL
     from tests import oracle_lib
-    N, T = 1500, 730
+    N, T = C3_WAVE_CELLS, C3_ROWS
     geo, xyz, vals = c3_region(N, T, nan_frac=0.01)
-    f = np.empty((5, T, N))
-    for var in range(5):
-        f[var] = oracle_idw(IDW_PARAMS[var][0], xyz, np.ascontiguousarray(vals[var]), geo[:, :3], C3_PARAMS[var],
-                            dst_slope=geo[:, 5])
+    idx = np.unique(np.concatenate([[0, N - 1], np.random.default_rng(2).choice(N, 1022, replace=False)]))
     p = synthetic.default_ptgsk_parameters()
     s = synthetic.default_ptgsk_state(N)
-    exp = oracle_lib.ptgsk_run(geo, p, s, synthetic.T0_2015_US, HOUR, f, full=True)
     r = HipRegion(PT_GS_K, N)
+    f_idx = np.empty((5, T, idx.size))
     try:
         r.set_geo(geo)
         r.set_parameters(p)
@@ -194,14 +253,20 @@ def test_c3_chain_idw_then_pt_gs_k_bitexact():
         r.set_state(s)
         for var in range(5):
             r.interpolate(var, xyz, np.ascontiguousarray(vals[var]), 0, C3_PARAMS[var])
-        got_f = np.stack([r.get_forcing(v, 0, T) for v in range(5)])
+            assert r.interpolation_path(var) == "wave"
+        for var in range(5):
+            exp_f = oracle_idw(IDW_PARAMS[var][0], xyz, np.ascontiguousarray(vals[var]), geo[:, :3], C3_PARAMS[var],
+                               dst_slope=geo[:, 5])
+            ok, msg = _same(r.get_forcing(var, 0, T), exp_f)
+            assert ok, f"forcing {var}: " + msg
+            f_idx[var] = exp_f[:, idx]
+            del exp_f
         r.run_cells(0, 0, T)
-        got = np.stack([r.get_series(k, 0, T) for k in range(8)])
-        st = r.get_state()
+        got = np.stack([r.get_series(k, 0, T)[:, idx] for k in range(8)])
+        st = r.get_state()[idx]
     finally:
         r.close()
-    ok, msg = _same(got_f, f)
-    assert ok, "forcing: " + msg
+    exp = oracle_lib.ptgsk_run(geo[idx], p, s[idx], synthetic.T0_2015_US, HOUR, f_idx, full=True)
     ok, msg = _same(got, exp["full"])
     assert ok, "series: " + msg
     assert np.array_equal(st, exp["state"])
