@@ -60,6 +60,14 @@ STACKS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launch", choices=("engine", "ranks"), default="engine",
+                    help="--gpus N > 1 without an outside launcher: 'engine' = this one process drives the N GPUs "
+                         "through a sharded region (shyft_hip_region_create_sharded: one shard per GPU, catchment / "
+                         "routing sums all-gathered by RCCL inside the engine); 'ranks' = start N rank processes "
+                         "(one per GPU, torch.distributed), as torch.distributed.run does")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="engine path: shards of the region (default: one per GPU); more shards than GPUs share "
+                         "devices round-robin (on one GPU: --gpus 1 --shards 2 runs two shards on device 0)")
     ap.add_argument("--steps", type=int, default=YEAR // CHUNK)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=0,
@@ -215,11 +223,12 @@ def _backend_name(pg):
     return "RCCL" if b == "nccl" else b
 
 
-def barrier_sync(pg, local):
+def barrier_sync(pg, local, devices=None):
     import torch
     if pg is not None:
         pg.barrier()
-    torch.cuda.synchronize(local)
+    for d in sorted(set(devices)) if devices else [local]:
+        torch.cuda.synchronize(d)
 
 
 def max_over_ranks(pg, local, v: float) -> float:
@@ -248,8 +257,16 @@ class Layout:
     Weak scaling (default): every rank owns --cells cells, 100 catchments per shard. Strong scaling
     (--total-cells): the region is split by distributed.shard_range."""
 
-    def __init__(self, a, world, rank):
+    def __init__(self, a, world, rank, engine_gpus=0):
         from shyft_amd import distributed
+        if engine_gpus:
+            # the engine path: this process owns the whole region (its shards spread it over the GPUs)
+            per = a.cells or (1 << 19 if a.stack == "hbv_stack" else 1 << 20)
+            self.total = a.total_cells or per * engine_gpus
+            self.off, self.n = 0, self.total
+            self.n_catch = a.catchments or (100 if a.total_cells else 100 * engine_gpus)
+            self.scaling = "strong" if a.total_cells else "weak"
+            return
         if a.total_cells:
             b, e = distributed.shard_range(a.total_cells, world, rank)
             self.off, self.n, self.total = b, e - b, a.total_cells
@@ -262,11 +279,11 @@ class Layout:
             self.scaling = "weak"
 
 
-def build_region(stack, L, local, chunk, n_steps_axis):
+def build_region(stack, L, local, chunk, n_steps_axis, devices=None):
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K, PT_HPS_K, COLLECT_DISCHARGE
     sid = {"pt_gs_k": PT_GS_K, "hbv_stack": HBV_STACK, "pt_ss_k": PT_SS_K, "pt_hs_k": PT_HS_K, "pt_hps_k": PT_HPS_K}[stack]
-    r = HipRegion(sid, L.n, device=local)
+    r = HipRegion(sid, L.n, device=local) if devices is None else HipRegion(sid, L.n, devices=devices)
     r.set_geo(synthetic.geo11(L.n, n_catchments=L.n_catch, cell_offset=L.off, n_total=L.total))
     r.set_parameters(stack_defaults(stack, 1)[0])
     r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, n_steps_axis, chunk)
@@ -503,7 +520,7 @@ PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
 def workload_tag(a, cells):
     """Key of a workload for the committed PMC summaries: they are only used for the exact same run."""
     return (f"{a.stack}{'_idw' if a.idw else ''}{'_btk' if a.btk else ''}_c{cells}_k{a.chunk}"
-            f"_s{a.steps}_w{a.warmup}")
+            f"_s{a.steps}_w{a.warmup}{f'_sh{a.shards}' if a.shards > 1 else ''}")
 
 
 def pmc_summary(a, cells):
@@ -557,20 +574,26 @@ def dist_check(a, world, rank, pg):
 
 def main():
     a = parse()
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    engine = "WORLD_SIZE" not in os.environ and a.launch == "engine" and not a.dist_check
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not engine:
         sys.exit(launch_ranks(a.gpus))
-    world, rank, local, pg = dist_setup(a.gpus, use_gpu=not a.dist_check)
+    devices = None
+    if engine and (a.gpus > 1 or a.shards > 1):
+        # one process, the region's cells in shards over the GPUs (the engine's multi-GPU path)
+        devices = [k % a.gpus for k in range(a.shards or a.gpus)]
+    world, rank, local, pg = dist_setup(1 if devices else a.gpus, use_gpu=not a.dist_check)
     if a.dist_check:
         return dist_check(a, world, rank, pg)
     import torch  # noqa: F401  (device init / sync)
     from shyft_amd import synthetic
 
-    L = Layout(a, world, rank)
-    cells = L.n
+    n_dev = len(set(devices)) if devices else world
+    L = Layout(a, world, rank, engine_gpus=n_dev if devices else 0)
+    cells = L.total // n_dev if devices else L.n      # per GPU (the shards of one GPU run concurrently)
     chunk = a.chunk
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
-    r = build_region(a.stack, L, local, chunk, n_axis)
-    state0 = stack_defaults(a.stack, cells)[1]
+    r = build_region(a.stack, L, local, chunk, n_axis, devices)
+    state0 = stack_defaults(a.stack, L.n)[1]
     read_b, write_b, state_b, kernel_name = STACKS[a.stack]
     stations = None
     if a.btk:
@@ -596,13 +619,13 @@ def main():
         run_year(r, L, chunk, a.warmup, synthetic.SEED, stations, router, a.btk, r_alt=r_alt, sums=sums,
                  overlap=a.overlap_forcing)
     r.set_state(state0)   # the initial state is an input: resident in HBM before the timed region
-    barrier_sync(pg, local)
+    barrier_sync(pg, local, devices)
     t0 = time.perf_counter()
     btk_ms = []
     walls, parts = [], []
     kernel_ms = run_year(r, L, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
                          r_alt=r_alt, sums=sums, walls=walls, parts=parts, overlap=a.overlap_forcing)
-    barrier_sync(pg, local)
+    barrier_sync(pg, local, devices)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
     avg_kernel_ms = max_over_ranks(pg, local, float(np.mean(kernel_ms)))
@@ -619,7 +642,7 @@ def main():
         "metric": METRIC if a.stack == "pt_gs_k" else METRIC.replace("pt_gs_k", a.stack),
         "value": value,
         "unit": "cell-steps/s",
-        "n_gpus": world,
+        "n_gpus": n_dev,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps,
@@ -647,9 +670,14 @@ def main():
                         "device generator, per chunk, overlapped with the previous chunk's run (two regions, state "
                         "handed over device to device)" if r_alt is not None else
                         "device generator, per chunk, before its run"),
-            "parallelism": f"cells sharded over {world} GPU(s), no data-path collective"
-                           + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered "
-                              f"({_backend_name(pg)}) and added in rank order"),
+            "parallelism": (f"one process, the region in {len(devices)} engine shards over {n_dev} GPU(s) "
+                            f"(shyft_hip_region_create_sharded), no data-path collective"
+                            + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered inside "
+                               f"the engine ({r.combine_path().upper()}) and added in shard order")
+                            if devices else
+                            f"cells sharded over {world} GPU(s), one process each, no data-path collective"
+                            + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered "
+                               f"({_backend_name(pg)}) and added in rank order")),
         },
         "kernel_ms_per_step": avg_kernel_ms,
         "kernel_cell_steps_per_s": L.total * chunk / (avg_kernel_ms * 1e-3),
@@ -683,10 +711,6 @@ def main():
             "ms_per_step": sum(walls[:ny]) / ny,
             "kernel_ms_per_step": float(np.mean(kernel_ms[:ny])),
             "note": "per-chunk wall clocks of this same timed run (synchronised at the end of each chunk)"}
-    if parts and len(parts[0]) == 2:
-        names = ("ptgsk_snow_kernel", "ptgsk_flux_kernel")
-        out["kernels"] = [{"name": names[k], "ms_per_step": float(np.mean([p[k] for p in parts])),
-                           "chunk_ms": [round(p[k], 2) for p in parts]} for k in range(2)]
     if a.btk:
         # the BTK time loop per chunk: one fp64 GEMM [cells x (S+3)] x [(S+3) x chunk], plus host
         # work (source rows, per-step beta); the full-set operators are built on the first chunk and reused
@@ -737,7 +761,7 @@ def main():
                                          "the timed region)"}
         if a.dump_sums and rank == 0:
             np.save(a.dump_sums, tot.cpu().numpy())
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not devices and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         out["cpu_baseline"] = cpu_baseline(a.stack, a.cpu_cells, threads)
     if rank == 0:

@@ -68,6 +68,22 @@ const char* shyft_hip_last_error(const shyft_hip_region* h);
  * device < 0 selects the current HIP device. */
 int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_region** out);
 void shyft_hip_region_destroy(shyft_hip_region* h);
+/* One region whose cells are split into n_shards contiguous shards, shard k (cells [n*k/S, n*(k+1)/S)) on device
+ * devices[k] -- devices may repeat (several shards on one device). Every entry point below works on the whole
+ * region as on an unsharded one (cell indexes, catchment ids and series are the region's); the shards run
+ * concurrently, one host thread per shard. This is region_model over all of a node's GPUs from one process
+ * (core/region_model.h:972-1021 runs the whole region in one process). Catchment / routing-group / ensemble sums
+ * add per-shard partial sums in shard order after an all-gather: RCCL (ncclAllGather over xGMI) when every shard
+ * has its own device, device-to-device copies when shards share one; a catchment whose cells lie in one shard sums
+ * exactly as on the unsharded region. Forcing and series move between host memory and the shards (no device
+ * pointers: each shard's memory is on its own device). */
+int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* devices, size_t n_shards,
+                                    shyft_hip_region** out);
+/* Number of shards (1 for an unsharded region); for k below it, shard k's device, first cell and cell count. */
+size_t shyft_hip_region_shards(const shyft_hip_region* h, size_t k, int* device, size_t* cell0, size_t* n_cells);
+/* How the shards' partial sums are combined: SHYFT_HIP_COMBINE_NONE (unsharded), _COPY (device copies), _RCCL. */
+enum shyft_hip_combine { SHYFT_HIP_COMBINE_NONE = 0, SHYFT_HIP_COMBINE_COPY = 1, SHYFT_HIP_COMBINE_RCCL = 2 };
+int shyft_hip_region_combine_path(const shyft_hip_region* h);
 size_t shyft_hip_region_size(const shyft_hip_region* h);
 
 /* Cell geometry, n_cells x 11 doubles in the geo_cell_data_io layout

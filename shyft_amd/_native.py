@@ -24,6 +24,9 @@ SIGNATURES = {
     "shyft_hip_last_error": (C.c_char_p, [_h]),
     "shyft_hip_region_create": (C.c_int, [C.c_int, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
     "shyft_hip_region_destroy": (None, [_h]),
+    "shyft_hip_region_create_sharded": (C.c_int, [C.c_int, C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "shyft_hip_region_shards": (C.c_size_t, [_h, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "shyft_hip_region_combine_path": (C.c_int, [_h]),
     "shyft_hip_region_size": (C.c_size_t, [_h]),
     "shyft_hip_set_geo": (C.c_int, [_h, C.c_void_p, C.c_void_p, C.c_void_p]),
     "shyft_hip_set_parameters": (C.c_int, [_h, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]),

@@ -15,10 +15,6 @@
 #include "special.h"
 #include "../include_internal/layout.h"
 
-// SHYFT_HBV_INT2: the snow step's two integrals in one walk over the bins (hbv_integrate0_2)
-#ifndef SHYFT_HBV_INT2
-#define SHYFT_HBV_INT2 1
-#endif
 
 namespace shyft_dev {
 
@@ -269,15 +265,11 @@ __device__ inline double hbv_snow_step(const hbv_snow_par_t<NB>& p, double (&sp)
         swe = 0.0;
     } else {
         const bool f_is_zero = sca >= 1.0 ? false : true;
-#if SHYFT_HBV_INT2
+        // the two integrals (swe = int sp + int sw over the same bins and limits) in one walk (hbv_integrate0_2)
         double a_sp, a_sw;
         hbv_integrate0_2(sp, sw, p.I, nb, sca, f_is_zero, a_sp, a_sw);
         swe = a_sp;
         swe += a_sw;
-#else
-        swe = hbv_integrate0(sp, p.I, nb, sca, f_is_zero);
-        swe += hbv_integrate0(sw, p.I, nb, sca, f_is_zero);
-#endif
     }
     if (total_water < swe) {
         if (total_water - swe < -1.0e-6) err = ERR_NEGATIVE_OUTFLOW;  // the reference throws (hbv_snow.h:259-263)

@@ -8,7 +8,7 @@
 namespace shyft_dev {
 
 // returns potential evapotranspiration in mm/s (priestley_taylor.h:75-102)
-__device__ SHYFT_INL_PT double pt_pot_evap(double albedo, double alpha, double temperature, double global_radiation,
+__device__ inline double pt_pot_evap(double albedo, double alpha, double temperature, double global_radiation,
                                      double rhumidity) {
     const bool neg = temperature < 0;
     const double ck2 = neg ? 17.84362 : 17.08085;
@@ -27,7 +27,7 @@ __device__ SHYFT_INL_PT double pt_pot_evap(double albedo, double alpha, double t
 
 // the same, plus exp(ae_arg) for the caller's actual_evapotranspiration in one dexp2 call with the saturation
 // pressure's exp (two independent exps side by side instead of back to back); the same bits as the two calls
-__device__ SHYFT_INL_PT double pt_pot_evap_exp(double albedo, double alpha, double temperature, double global_radiation,
+__device__ inline double pt_pot_evap_exp(double albedo, double alpha, double temperature, double global_radiation,
                                          double rhumidity, double ae_arg, double& ae_exp) {
     const bool neg = temperature < 0;
     const double ck2 = neg ? 17.84362 : 17.08085;

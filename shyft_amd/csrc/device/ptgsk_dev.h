@@ -11,15 +11,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "fastmath.h"
 #include "pt_dev.h"
 #include "special.h"
 #include "../include_internal/layout.h"
 
-// SHYFT_GS_EXP2: the energy balance's two independent exps in one dexp2 call (gs step, below)
-#ifndef SHYFT_GS_EXP2
-#define SHYFT_GS_EXP2 1
-#endif
 
 namespace shyft_dev {
 
@@ -48,7 +43,7 @@ struct gs_lw {
 };
 
 // gamma_snow.h:230-260
-__device__ SHYFT_INL_SNOW void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
+__device__ inline void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
                                        double max_water_frac, double temp_swe, double& swe, double& sca,
                                        lgamma_cache& lgc, gs_lw& lw) {
     lw.p = lw.p1 = __builtin_nan("");
@@ -91,18 +86,6 @@ __device__ inline double gs_calc_q(double a, double b, double z, double lga) {
     return a * b * g.p1 + z * (1.0 - g.p);
 }
 
-// the same with every elementary function inlined (the Brent solver's f, SHYFT_BRENT_INL)
-__device__ __forceinline__ double gs_calc_q_inl(double a, double b, double z, double lga) {
-    const gamma_p_result g = gamma_p_prefix_inl(a, z / b, lga, detmath::gamma_snow_policy_eps(a));
-    return a * b * g.p1 + z * (1.0 - g.p);
-}
-#ifndef SHYFT_BRENT_INL
-#define SHYFT_BRENT_INL 0
-#endif
-// SHYFT_BRENT_ATTR: the Brent job as an out-of-line call (default) or inlined into the step loop
-#ifndef SHYFT_BRENT_ATTR
-#define SHYFT_BRENT_ATTR __noinline__
-#endif
 
 // corr_lwc (gamma_snow.h:214-227): boost brent_find_minima over [0, z1],
 // 12 bits, 60 iterations; golden constant is the float literal 0.3819660f.
@@ -115,7 +98,7 @@ __device__ __forceinline__ double gs_calc_q_inl(double a, double b, double z, do
 // else NaN
 // lga2 = lgamma(a2): the job's lane evaluates it (its lgamma cache needs it for the step's calc_snow_state after
 // the solve anyway), so the solving wavefront does not
-__device__ SHYFT_BRENT_ATTR double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2,
+__device__ __noinline__ double gs_corr_lwc(double z1, double a1, double b1, double a2, double b2,
                                            double q1, double lga2 SHYFT_PROF_NF) {
 #ifdef SHYFT_ABLATE_BRENT
     return z1 * 0.5;  // timing ablation only (wrong results)
@@ -125,11 +108,7 @@ __device__ SHYFT_BRENT_ATTR double gs_corr_lwc(double z1, double a1, double b1, 
 #ifdef SHYFT_PROF
         ++nf_evals;
 #endif
-#if SHYFT_BRENT_INL
-        const double v = gs_calc_q_inl(a2, b2, z, lga2) - Q1;
-#else
         const double v = gs_calc_q(a2, b2, z, lga2) - Q1;
-#endif
         return v * v;
     };
     double min = 0.0, max = z1;
@@ -219,7 +198,7 @@ struct gs_carry {
     bool ok = false;
 };
 
-__device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
+__device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
                                       const double* __restrict__ P, const gs_cell& cc, double T, double rad,
                                       double prec_mm_h, double wind_speed, double rel_hum, lgamma_cache& lgc,
                                       const gs_carry& carry) {
@@ -265,13 +244,9 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
 
     const double sigma = 5.670373e-8;
     double effect = rad * (1.0 - albedo);
-#if SHYFT_GS_EXP2
     // dpowr(vapour_pressure / T_k, 6.87e-2)'s exp and the sub-zero surface branch's exp in one dexp2 call
     const dexp_pair gse = dexp2(6.87e-2 * dlog(vapour_pressure / T_k), 0.103 * T - 0.186);
     effect += 0.98 * sigma * gse.a * dpow4(T_k);
-#else
-    effect += 0.98 * sigma * dpowr(vapour_pressure / T_k, 6.87e-2) * dpow4(T_k);
-#endif
     if (T > 0.0 && snow < GS_TOL) effect += rain * T * 4180.0 / dt_s;
     if (T <= 0.0 && rain < GS_TOL) effect += snow * T * 2050.0 / dt_s;
 
@@ -283,11 +258,7 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
     if (sst > -GS_TOL)
         effect += turb * (T + 1.7 * (vapour_pressure - 6.12)) - P[PK_BB0];
     else
-#if SHYFT_GS_EXP2
         effect += turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * gse.b)) -
-#else
-        effect += turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * dexp(0.103 * T - 0.186))) -
-#endif
                   0.98 * sigma * dpow4(sst + 273.15);
 
     double delta_sh = -surface_heat;
@@ -347,7 +318,7 @@ __device__ SHYFT_INL_GS void gs_front(const gs_state& s, gs_mid& m, bool start_m
     m.sdc_scale = sdc_scale;
 }
 
-__device__ SHYFT_INL_GS void gs_back(gs_state& s, const gs_mid& m, double z, double& r_sca, double& r_storage,
+__device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r_sca, double& r_storage,
                                      double& r_outflow, bool snow_season, double dt_us, const double* __restrict__ P,
                                      const gs_cell& cc, double prec_mm_h, lgamma_cache& lgc, gs_carry& carry) {
     if (m.done) {
@@ -447,35 +418,12 @@ __device__ inline double gs_solve_lwc(const gs_mid& m) {
 }
 
 // ------------------------------------------------------------------ kirchner
-// SHYFT_K_FM: kirchner's exps inline with their constants in SGPRs (device/fastmath.h), loaded once per step
-#ifndef SHYFT_K_FM
-#define SHYFT_K_FM 0
-#endif
-#if SHYFT_K_FM
-#define K_EXP(x) fm_exp((x), ek)
-#define K_EXP_DECL const fm_exp_k ek = fm_exp_load();
-#define K_EXP_ARG , const fm_exp_k& ek
-#define K_EXP_PASS , ek
-#else
-#define K_EXP(x) dexp(x)
-#define K_EXP_DECL
-#define K_EXP_ARG
-#define K_EXP_PASS
-#endif
 // kirchner.h:186-198
-// SHYFT_K_EXP2: both of kirchner_f's exps in one dexp2 call (exp(-ln_q) is evaluated even when g < 1e-30 does
-// not use it; the value is the same either way)
-#ifndef SHYFT_K_EXP2
-#define SHYFT_K_EXP2 1
-#endif
-__device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, double c2, double c3 K_EXP_ARG) {
-#if SHYFT_K_EXP2 && !SHYFT_K_FM
+// both of kirchner_f's exps in one dexp2 call (exp(-ln_q) is evaluated even when g < 1e-30 does not use it; the
+// value is the same either way)
+__device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, double c2, double c3) {
     const dexp_pair ge = dexp2(c1 + c2 * ln_q + c3 * ln_q * ln_q, -ln_q);
     return ge.a >= 1.e-30 ? ge.a * (p_minus_e * ge.b - 1.0) : 0.0;
-#else
-    const double g = K_EXP(c1 + c2 * ln_q + c3 * ln_q * ln_q);
-    return g >= 1.e-30 ? g * (p_minus_e * K_EXP(-ln_q) - 1.0) : 0.0;
-#endif
 }
 
 // kirchner::calculator::step with trapezoidal_average (kirchner.h:23-53, 213-235).
@@ -483,17 +431,16 @@ __device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, do
 // accepted) is flattened into one loop of try_steps so lanes of a wave that
 // need different numbers of attempts stay in one convergent loop.
 // Returns false if a do_step needed 500 attempts (odeint failed_step_checker).
-__device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, double e, double t1, double c1, double c2,
+__device__ inline bool kirchner_step(double& q, double& q_avg, double p, double e, double t1, double c1, double c2,
                                      double c3) {
     const double abs_err = 1.0e-7, rel_err = 1.0e-8;
-    K_EXP_DECL
     if (q < 0.00001) q = 0.00001;
 #ifdef SHYFT_ABLATE_KIRCHNER
     q_avg = q; q = q + 0.01 * (p - e); return true;  // timing ablation only (wrong results)
 #endif
     const double pe = p - e;
     double x = dlog(q);
-    double dxdt = kirchner_f(x, pe, c1, c2, c3 K_EXP_PASS);
+    double dxdt = kirchner_f(x, pe, c1, c2, c3);
     double t = 0.0, dt = t1;
     double x_old = x, dxdt_old = dxdt, t_old = 0.0;
     double k3 = 0, k4 = 0, k5 = 0, k6 = 0;
@@ -511,21 +458,21 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
                  dc5 = c5_ - -92097.0 / 339200, dc6 = c6_ - 187.0 / 2100, dc7 = -1.0 / 40;
     while (t < t1) {
         double xt = 1.0 * x + dt * b21 * dxdt;
-        const double k2 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
+        const double k2 = kirchner_f(xt, pe, c1, c2, c3);
         xt = 1.0 * x + dt * b31 * dxdt + dt * b32 * k2;
-        const double s3 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
+        const double s3 = kirchner_f(xt, pe, c1, c2, c3);
         xt = 1.0 * x + dt * b41 * dxdt + dt * b42 * k2 + dt * b43 * s3;
-        const double s4 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
+        const double s4 = kirchner_f(xt, pe, c1, c2, c3);
         xt = 1.0 * x + dt * b51 * dxdt + dt * b52 * k2 + dt * b53 * s3 + dt * b54 * s4;
-        const double s5 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
+        const double s5 = kirchner_f(xt, pe, c1, c2, c3);
         xt = 1.0 * x + dt * b61 * dxdt + dt * b62 * k2 + dt * b63 * s3 + dt * b64 * s4 + dt * b65 * s5;
-        const double s6 = kirchner_f(xt, pe, c1, c2, c3 K_EXP_PASS);
+        const double s6 = kirchner_f(xt, pe, c1, c2, c3);
         const double xo = 1.0 * x + dt * c1_ * dxdt + dt * c3_ * s3 + dt * c4_ * s4 + dt * c5_ * s5 + dt * c6_ * s6;
-        const double dxdt_o = kirchner_f(xo, pe, c1, c2, c3 K_EXP_PASS);
+        const double dxdt_o = kirchner_f(xo, pe, c1, c2, c3);
         const double xerr = dt * dc1 * dxdt + dt * dc3 * s3 + dt * dc4 * s4 + dt * dc5 * s5 + dt * dc6 * s6 + dt * dc7 * dxdt_o;
         const double err = fabs(xerr) / (abs_err + rel_err * (1.0 * fabs(x) + 1.0 * dt * fabs(dxdt)));
         if (err > 1.0) {
-            dt = dt * smax(0.9 * K_EXP(-1.0 / 3.0 * dlog(err)), 1.0 / 5.0);  // dpowr(err, -1/3)
+            dt = dt * smax(0.9 * dexp(-1.0 / 3.0 * dlog(err)), 1.0 / 5.0);  // dpowr(err, -1/3)
             if (++attempts >= 500) { ok = false; break; }
             continue;
         }
@@ -536,13 +483,13 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         // from dt = t1), so the log + exp of the controller are skipped on the call's last step
         if (err < 0.5 && t < t1) {
             const double e2 = smax(0.00032, err);  // dpow(5.0, -5.0)
-            dt = dt * (9.0 / 10.0 * K_EXP(-1.0 / 5.0 * dlog(e2)));  // dpowr(e2, -1/5)
+            dt = dt * (9.0 / 10.0 * dexp(-1.0 / 5.0 * dlog(e2)));  // dpowr(e2, -1/5)
         }
         x_old = x; dxdt_old = dxdt;
         x = xo; dxdt = dxdt_o;
         k3 = s3; k4 = s4; k5 = s5; k6 = s6;
         if (t < t1) {
-            const double fv = K_EXP(x);
+            const double fv = dexp(x);
             area += 0.5 * (f_a + fv) * (t - t_a);
             f_a = fv;
             t_a = t;
@@ -574,7 +521,7 @@ __device__ SHYFT_INL_K bool kirchner_step(double& q, double& q_avg, double p, do
         x = 1.0 * x_old + h * b1_theta * dxdt_old + h * b3_theta * k3 + h * b4_theta * k4 + h * b5_theta * k5 +
             h * b6_theta * k6 + h * b7_theta * dxdt;
     }
-    q = K_EXP(x);
+    q = dexp(x);
     area += 0.5 * (f_a + q) * (t1 - t_a);
     q_avg = area / (t1 - 0.0);
     return ok;

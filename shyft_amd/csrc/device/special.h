@@ -21,49 +21,10 @@ namespace shyft_dev {
 
 __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
-// inlining policy of the heavy device functions (tuned for VGPR pressure / I-cache)
-#ifndef SHYFT_INL_SNOW
-#define SHYFT_INL_SNOW inline
-#endif
-#ifndef SHYFT_INL_GS
-#define SHYFT_INL_GS inline
-#endif
-#ifndef SHYFT_INL_K
-#define SHYFT_INL_K inline
-#endif
-#ifndef SHYFT_INL_PT
-#define SHYFT_INL_PT inline
-#endif
-#ifndef SHYFT_INL_GP
-#define SHYFT_INL_GP inline
-#endif
-#ifndef SHYFT_DM_INLINE
-#define SHYFT_DM_INLINE __noinline__
-#endif
-#ifndef SHYFT_DM_INLINE_POW
-#define SHYFT_DM_INLINE_POW __noinline__
-#endif
-// SHYFT_DM_SGPR: the out-of-line exp / log take their polynomial coefficients as SGPR operands of v_fma_f64
-// (s_mov pairs on the scalar unit) instead of the compiler's v_mov_b32 pair per coefficient (dm_sgpr.h)
-#ifndef SHYFT_DM_SGPR
-#define SHYFT_DM_SGPR 0
-#endif
-#if SHYFT_DM_SGPR
-}  // namespace shyft_dev
-#include "dm_sgpr.h"
-namespace shyft_dev {
-__device__ SHYFT_DM_INLINE double dexp(double x) { return dm_exp_s(x); }
-#else
-__device__ SHYFT_DM_INLINE double dexp(double x) { return detmath::exp(x); }
-#endif
-#ifndef SHYFT_DM_INLINE_LOG
-#define SHYFT_DM_INLINE_LOG SHYFT_DM_INLINE
-#endif
-#if SHYFT_DM_SGPR
-__device__ SHYFT_DM_INLINE_LOG double dlog(double x) { return dm_log_s(x); }
-#else
-__device__ SHYFT_DM_INLINE_LOG double dlog(double x) { return detmath::log(x); }
-#endif
+// the elementary functions are out-of-line device functions (one copy each: I-cache and register pressure of the
+// step loops), the physics around them is inlined
+__device__ __noinline__ double dexp(double x) { return detmath::exp(x); }
+__device__ __noinline__ double dlog(double x) { return detmath::log(x); }
 // two exps in one out-of-line call: the two Horner chains interleave (each one's fma latency hidden behind the
 // other's), where two calls would run them back to back; the same bits as two dexp calls
 struct dexp_pair {
@@ -99,7 +60,7 @@ __device__ __noinline__ dexp_pair dexp2(double x, double y) {
     }
     return r;
 }
-__device__ SHYFT_DM_INLINE_POW double dpow(double x, double y) { return detmath::pow(x, y); }
+__device__ __noinline__ double dpow(double x, double y) { return detmath::pow(x, y); }
 __device__ __noinline__ double dlgamma(double x) { return detmath::lgamma(x); }
 // structured powers (detmath::pow4 / pow8 / powr, the oracle's OPOW4 / OPOW8 / OPOWR)
 __device__ __forceinline__ double dpow4(double x) { return detmath::pow4(x); }
@@ -114,25 +75,15 @@ struct dev_math {
     __device__ static double log(double x) { return dlog(x); }
 };
 using gamma_p_result = detmath::gamma_pq_result;
-// the same functions forced inline: for leaf solvers (the Brent job of gamma_snow), where an out-of-line call would
-// cost its ABI entry wait (s_waitcnt on every outstanding memory operation) in the middle of a dependent chain
-struct dev_math_inl {
-    __device__ static __forceinline__ double exp(double x) { return detmath::exp(x); }
-    __device__ static __forceinline__ double log(double x) { return detmath::log(x); }
-};
-
 // lga = lgamma(a) supplied by the caller (shape changes rarely, so callers cache it);
 // eps = the relative termination tolerance (boost precision policy of the caller)
-__device__ SHYFT_INL_GP gamma_p_result gamma_p_prefix(double a, double x, double lga, double eps) {
+__device__ inline gamma_p_result gamma_p_prefix(double a, double x, double lga, double eps) {
 #ifdef SHYFT_ABLATE_GAMMA
     gamma_p_result r; r.p = 0.5; r.p1 = 0.4; r.prefix = 0.01; return r;  // timing ablation only (wrong results)
 #endif
     return detmath::gamma_pq<dev_math>(a, x, lga, eps);
 }
 
-__device__ __forceinline__ gamma_p_result gamma_p_prefix_inl(double a, double x, double lga, double eps) {
-    return detmath::gamma_pq<dev_math_inl>(a, x, lga, eps);
-}
 
 // gamma_snow's calls: boost precision policy by shape (gamma_snow.h:195-197)
 __device__ inline gamma_p_result gs_gamma_pq(double a, double x, double lga) {

@@ -237,12 +237,17 @@ class region_model {
     using state_t = std::vector<double>;
 
     // region_model(const vector<geo_cell_data>&, const parameter_t&)  (region_model.h:285-293)
+    // devices: the region's cells in contiguous shards, one per entry (repeats allowed), all driven from this process
+    // (shyft_hip_region_create_sharded); empty: one region on `device`
     region_model(const std::vector<geo_cell_data>& geov, const parameter_t& region_param, bool full_collection = true,
-                 int device = -1)
+                 int device = -1, const std::vector<int>& devices = {})
         : geo_(geov), full_(full_collection) {
         if (geo_.empty()) throw std::runtime_error("region_model: no cells");
         shyft_hip_region* h = nullptr;
-        throw_if(shyft_hip_region_create(Stack::id, geo_.size(), device, &h), nullptr);
+        if (devices.empty())
+            throw_if(shyft_hip_region_create(Stack::id, geo_.size(), device, &h), nullptr);
+        else
+            throw_if(shyft_hip_region_create_sharded(Stack::id, geo_.size(), devices.data(), devices.size(), &h), nullptr);
         h_.reset(h, shyft_hip_region_destroy);
         ncore = std::max(1u, std::thread::hardware_concurrency());
         state_collection_.assign(geo_.size(), false);
@@ -256,8 +261,9 @@ class region_model {
     }
     // region_model(cells, region_param, catchment_parameters)  (region_model.h:294-301)
     region_model(const std::vector<geo_cell_data>& geov, const parameter_t& region_param,
-                 const std::map<int64_t, parameter_t>& catchment_parameters, bool full_collection = true)
-        : region_model(geov, region_param, full_collection) {
+                 const std::map<int64_t, parameter_t>& catchment_parameters, bool full_collection = true,
+                 const std::vector<int>& devices = {})
+        : region_model(geov, region_param, full_collection, -1, devices) {
         for (const auto& kv : catchment_parameters) set_catchment_parameter(kv.first, kv.second);
     }
     // copy ctor / clone (region_model.h:297, clone :256-276): a true deep copy, device data included;
@@ -278,6 +284,12 @@ class region_model {
     river_network rivers;
 
     shyft_hip_region* handle() const { return h_.get(); }
+    // the device of each shard (one entry for an unsharded region)
+    std::vector<int> shard_devices() const {
+        std::vector<int> d(shyft_hip_region_shards(h_.get(), 0, nullptr, nullptr, nullptr));
+        for (size_t k = 0; k < d.size(); ++k) shyft_hip_region_shards(h_.get(), k, &d[k], nullptr, nullptr);
+        return d;
+    }
     bool full_collection() const { return full_; }
     size_t size() const { return geo_.size(); }
     const std::vector<geo_cell_data>& cells_geo() const { return geo_; }

@@ -29,16 +29,9 @@ struct ptgsk_kargs {
     double* state_series;          // [PTGSK_NS][win_len+1][N] or null
     const uint8_t* active;         // [N] catchment filter or null
     int32_t* err;                  // [N]
-    double* hand;                  // [2][win_len][N] snow -> flux hand-over (gs sca, gs outflow), split launch
 };
 
-// SHYFT_PTGSK_SPLIT: run_cells of pt_gs_k as two kernels (gamma_snow, then the flux methods) with an HBM hand-over
-// instead of the fused step kernel. Measured slower, so off; kept for the record and for variants.
-#ifndef SHYFT_PTGSK_SPLIT
-#define SHYFT_PTGSK_SPLIT 0
-#endif
-// split launch (snow kernel, then flux kernel): ev_mid, if given, is recorded between the two
-hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t ev_mid = nullptr);
+hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream);
 
 struct hbv_kargs {
     int n_cells, step0, n_steps, win0, win_len, collect;
@@ -133,6 +126,11 @@ hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_step
 hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
                                const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream,
                                const double* w = nullptr);
+// sharded regions: a shard's [n_rows][n] partials into rows[r] of the region's [R][n]; S partials [S][M] added in
+// shard order
+hipError_t launch_scatter_rows(const double* src, const int32_t* rows, size_t n_rows, size_t n, double* dst,
+                               hipStream_t stream);
+hipError_t launch_ordered_sum(const double* g, size_t S, size_t M, double* out, hipStream_t stream);
 
 // dst[r][l] = src[r][idx[l]] for r < n_rows, l < n_lanes (parameter-ensemble lane replication)
 hipError_t launch_gather_columns(double* dst, const double* src, size_t n_rows, size_t src_cols, const int32_t* idx,

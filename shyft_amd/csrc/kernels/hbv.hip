@@ -21,55 +21,32 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-// forcing prefetch depth: steps i+1 .. i+D are in flight while step i computes. The kernel moves 48 B per
-// cell-step and does little arithmetic per byte, so its HBM rate is set by the bytes in flight (Little's law):
-// at 2 waves per SIMD one step ahead keeps ~16 KB per CU in flight.
-#ifndef SHYFT_HBV_PF
-#define SHYFT_HBV_PF 1
-#endif
+// forcing prefetch depth: step i+1's forcing is in flight while step i computes. The kernel moves 48 B per
+// cell-step and does little arithmetic per byte, so its HBM rate is set by the bytes in flight (Little's law).
+// Depths 2-4, LDS-resident bin arrays and nontemporal loads/stores measured no better.
+constexpr int PREFETCH = 1;
 
-// occupancy target (waves per SIMD; variant builds override with -DSHYFT_HBV_WAVES=N, 0 = the compiler's choice)
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_HBV_WAVES=N). Measured (512K cells, ms
+// per 730-step chunk, year mean): per-lane parameter rows: 2 waves 15.0, 3: 16.3, 4: 23.1; uniform rows in SGPRs
+// (the default launch): 2: 13.8, 3: 11.5, 4: 11.0, 5: 17.6.
 #ifndef SHYFT_HBV_WAVES
-// measured (512K cells, ms per 730-step chunk, year mean): per-lane parameter rows: 2 waves 15.0, 3: 16.3,
-// 4: 23.1; uniform rows in SGPRs (the default launch): 2: 13.8, 3: 11.5, 4: 11.0, 5: 17.6. Prefetch depth 1-4
-// and LDS-resident bin arrays measured no better.
 #define SHYFT_HBV_WAVES 4
 #endif
-#ifndef SHYFT_HBV_WAVES_PERLANE
-#define SHYFT_HBV_WAVES_PERLANE 2  // the per-lane-parameter launch (catchment parameter sets)
-#endif
-#define SHYFT_HBV_OCC __attribute__((amdgpu_waves_per_eu(UNIFORM ? SHYFT_HBV_WAVES : SHYFT_HBV_WAVES_PERLANE, \
-                                                         UNIFORM ? SHYFT_HBV_WAVES : SHYFT_HBV_WAVES_PERLANE)))
+constexpr int WAVES_PERLANE = 2;  // the per-lane-parameter launch (catchment parameter sets)
 
 // UNIFORM: every cell uses parameter set 0, so the parameter row (incl. the bin distribution s[], I[]) is
 // wave-uniform and lives in SGPRs instead of 2 x 8 + 15 per-lane doubles of VGPRs
 // NB: register capacity of the bin arrays (HBV_MAX_BINS, or 5 when every parameter set has at most 5 bins and
 // no state series is collected: 10.9 -> 9.4 ms per 512K-cell chunk). Bins NB..HBV_MAX_BINS-1 of the state in
 // HBM are then written as zeros, as the oracle's state vector (nb entries, padded) reads back.
-// streaming hints for the read-once forcing and write-once responses (variant builds: -DSHYFT_HBV_NT=1)
-#ifndef SHYFT_HBV_NT
-#define SHYFT_HBV_NT 0
-#endif
-#ifndef SHYFT_HBV_POW2
-#define SHYFT_HBV_POW2 1
-#endif
-#ifndef SHYFT_HBV_PRELOAD
-#define SHYFT_HBV_PRELOAD 0
-#endif
-#if SHYFT_HBV_NT
-#define HBV_LD(p) __builtin_nontemporal_load(&(p))
-#define HBV_ST(p, v) __builtin_nontemporal_store((v), &(p))
-#else
-#define HBV_LD(p) (p)
-#define HBV_ST(p, v) ((p) = (v))
-#endif
-
 // LEAN: the instance for the common launch (discharge collector only, no state series, no ensemble forcing columns):
 // those paths and their
 // pointers are compiled out, which keeps the step loop's scalar registers (the uniform parameter row, the series
 // bases) within the SGPR file instead of spilled to VGPR lanes (a v_readlane_b32, VALU issue, per use)
 template <bool UNIFORM, int NB, bool LEAN = false>
-__global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_kargs a) {
+__global__ __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(UNIFORM ? SHYFT_HBV_WAVES : WAVES_PERLANE, UNIFORM ? SHYFT_HBV_WAVES : WAVES_PERLANE)))
+void hbv_run_kernel(const hbv_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;
@@ -78,38 +55,6 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     const size_t NF = !LEAN && a.fcol ? (size_t)a.f_cols : N;
     const size_t fcl = !LEAN && a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
     const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * HBV_NP;
-#if SHYFT_HBV_PRELOAD
-    // the uniform parameter row is read again in every step (scalar loads, constant-cache hits) instead of held
-    // in SGPRs across the time loop: the row (22 values + 2 x NB bin values) does not fit next to the loop's own
-    // SGPRs, and the compiler's SGPR spills to VGPR lanes cost a v_readlane_b32 (VALU issue) per use
-#define HBV_PARAMS()                                                                        \
-    const double* __restrict__ Pq = P;                                                      \
-    if (UNIFORM) asm volatile("" : "+s"(Pq));                                               \
-    hbv_snow_par_t<NB> sp_par;                                                              \
-    sp_par.nb = (int)Pq[HK_NB];                                                             \
-    _Pragma("unroll") for (int i_ = 0; i_ < NB; ++i_) {                                     \
-        sp_par.s[i_] = Pq[HK_S0 + i_];                                                      \
-        sp_par.I[i_] = Pq[HK_I0 + i_];                                                      \
-    }                                                                                       \
-    sp_par.tx = Pq[HK_TX]; sp_par.cx = Pq[HK_CX]; sp_par.ts = Pq[HK_TS]; sp_par.lw = Pq[HK_LW]; \
-    sp_par.cfr = Pq[HK_CFR];                                                                \
-    const double fc = Pq[HK_FC], beta = Pq[HK_BETA], lp = Pq[HK_LP];                        \
-    const double uz1 = Pq[HK_UZ1], kuz2 = Pq[HK_KUZ2], kuz1 = Pq[HK_KUZ1], perc = Pq[HK_PERC], klz = Pq[HK_KLZ]; \
-    const double p_corr = Pq[HK_PCORR], pt_albedo = Pq[HK_PT_ALBEDO], pt_alpha = Pq[HK_PT_ALPHA], dtf = Pq[HK_DTF]; \
-    const double gm_direct = Pq[HK_GM_DIRECT];                                              \
-    const double gm_routed = 1 - gm_direct;
-    hbv_snow_par_t<NB> sp_par0;
-    sp_par0.nb = (int)P[HK_NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-        sp_par0.s[i] = P[HK_S0 + i];
-        sp_par0.I[i] = P[HK_I0 + i];
-    }
-    sp_par0.tx = P[HK_TX]; sp_par0.cx = P[HK_CX]; sp_par0.ts = P[HK_TS]; sp_par0.lw = P[HK_LW]; sp_par0.cfr = P[HK_CFR];
-#define sp_par_init sp_par0
-#else
-#define HBV_PARAMS()
-#define sp_par_init sp_par
     hbv_snow_par_t<NB> sp_par;
     sp_par.nb = (int)P[HK_NB];
 #pragma unroll
@@ -127,7 +72,6 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     const double p_corr = P[HK_PCORR], pt_albedo = P[HK_PT_ALBEDO], pt_alpha = P[HK_PT_ALPHA], dtf = P[HK_DTF];
     const double gm_direct = P[HK_GM_DIRECT];
     const double gm_routed = 1 - gm_direct;
-#endif
 
     const double* __restrict__ cc = a.cellc;
     const double glacier_fraction = cc[HC_GLACIER * N + cell];
@@ -151,9 +95,9 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         sw[i] = i < nbs ? st[(HS_SW0 + i) * N + cell] : 0.0;
     }
     // state.snow.distribute(parameter.snow, false) (hbv_stack.h:310): only on a bin-count mismatch
-    if ((int)nb_state != sp_par_init.nb) {
-        hbv_distribute(sp_par_init, sp, sw, swe, sca);
-        nb_state = (double)sp_par_init.nb;
+    if ((int)nb_state != sp_par.nb) {
+        hbv_distribute(sp_par, sp, sw, swe, sca);
+        nb_state = (double)sp_par.nb;
     }
     int32_t err = 0;
 
@@ -185,18 +129,17 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
     const int i_end = a.step0 + a.n_steps;
     // the next D steps' forcing is loaded before this step's arithmetic, so its HBM latency overlaps D steps
     // instead of stalling the top of every iteration
-    constexpr int D = SHYFT_HBV_PF;
+    constexpr int D = PREFETCH;
     double rt[D], rr[D], rh[D], rp[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         rt[k] = rr[k] = rh[k] = rp[k] = 0.0;
         if (a.step0 + k < i_end) {
             const size_t ff = (size_t)(a.step0 + k - a.win0) * NF + fcl;
-            rt[k] = HBV_LD(f_temp[ff]); rr[k] = HBV_LD(f_rad[ff]); rh[k] = HBV_LD(f_rh[ff]); rp[k] = HBV_LD(f_prec[ff]);
+            rt[k] = f_temp[ff]; rr[k] = f_rad[ff]; rh[k] = f_rh[ff]; rp[k] = f_prec[ff];
         }
     }
     for (int i = a.step0; i < i_end; ++i) {
-        HBV_PARAMS()
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
         const double temp = rt[0], rad = rr[0], rel_hum = rh[0], prec_raw = rp[0];
@@ -206,7 +149,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         }
         if (i + D < i_end) {
             const size_t fn = (wi + D) * NF + fcl;
-            rt[D - 1] = HBV_LD(f_temp[fn]); rr[D - 1] = HBV_LD(f_rad[fn]); rh[D - 1] = HBV_LD(f_rh[fn]); rp[D - 1] = HBV_LD(f_prec[fn]);
+            rt[D - 1] = f_temp[fn]; rr[D - 1] = f_rad[fn]; rh[D - 1] = f_rh[fn]; rp[D - 1] = f_prec[fn];
         }
         const double prec = prec_raw * p_corr;
         if (SS) collect_state(wi);
@@ -232,14 +175,10 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         // hbv_soil::step (hbv_soil.h:55-64)
         const double soil_temp = sm + snow_outflow;
-#if SHYFT_HBV_POW2
         // detmath::pow returns x * x for y == 2 (the default beta): beta is wave-uniform with one parameter set, so
         // this takes a scalar branch instead of a call (whose entry would wait for the prefetched forcing)
         const double soil_x = soil_temp / fc;
         const double soil_q = snow_outflow * (beta == 2.0 ? soil_x * soil_x : dpow(soil_x, beta));
-#else
-        const double soil_q = snow_outflow * dpow(soil_temp / fc, beta);
-#endif
         const double soil_outflow = soil_q > soil_temp ? soil_temp : soil_q;
         sm = smax(0.0, sm + snow_outflow - soil_outflow - ae);
         // hbv_tank::step (hbv_tank.h:64-80)
@@ -257,8 +196,8 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
         const double charge_m3s = +(cell_area_m2 * prec * mmh_to_m3s_scale_factor) -
                                   (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
-        HBV_ST(R[HR_AVG_DISCHARGE * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
-        HBV_ST(R[HR_CHARGE_M3S * RS + fo], charge_m3s);
+        R[HR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
+        R[HR_CHARGE_M3S * RS + fo] = charge_m3s;
         if (!LEAN && a.collect >= 1) {
             // response.snow.snow_state is never written by hbv_snow::step (hbv_snow.h:121-124): the
             // reference collects its default (swe = sca = 0)
@@ -296,9 +235,7 @@ __global__ __launch_bounds__(BLOCK) SHYFT_HBV_OCC void hbv_run_kernel(const hbv_
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    static const char* lean_env = getenv("SHYFT_HBV_LEAN");  // measurement knob: "0" = the general 5-bin instance
-    const bool lean = !lean_env || lean_env[0] != '0';
-    if (a.uniform_params && a.nb_max <= 5 && !a.state_series && !a.fcol && a.collect == 0 && lean)
+    if (a.uniform_params && a.nb_max <= 5 && !a.state_series && !a.fcol && a.collect == 0)
         hipLaunchKernelGGL((hbv_run_kernel<true, 5, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
         hipLaunchKernelGGL((hbv_run_kernel<true, 5>), dim3(grid), dim3(BLOCK), 0, stream, a);

@@ -24,16 +24,11 @@ namespace {
 
 constexpr int KMAX = IDW_KMAX;
 
-#ifndef SHYFT_IDW_DZREG
-#define SHYFT_IDW_DZREG 1
-#endif
-// SHYFT_IDW_WAVE: gathers through the wavefront's union of neighbour stations when every wavefront's union fits 64
-#ifndef SHYFT_IDW_WAVE
-#define SHYFT_IDW_WAVE 1
-#endif
-#ifndef SHYFT_IDW_LDS_KB
-#define SHYFT_IDW_LDS_KB 32
-#endif
+// the temperature gather (without gradient_by_equation) keeps each neighbour's d.z - s.z in a register (the
+// neighbour table's aux column), not the station coordinates in LDS
+constexpr bool DZREG = true;
+// LDS budget of the row-tile gather's source tiles (60 KB measured slower)
+constexpr size_t LDS_KB = 32;
 
 __global__ __launch_bounds__(128) void idw_neighbours_kernel(idw_nb_args a) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,10 +116,10 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
     const int S = a.n_sources;
     const int kept = a.count[j];
     const double slope = KIND == IDW_RADIATION ? (a.slope ? a.slope[j] : 0.9) : 0.0;
-    // LDS layout: [src x | src y | src z] (temperature with gradient_by_equation, or without SHYFT_IDW_DZREG) then
+    // LDS layout: [src x | src y | src z] (temperature with gradient_by_equation, or without DZREG) then
     // the row tile; otherwise the coordinates are read from global memory where they are still needed (once per
     // lane, and by the general scan of a row with a non-finite value)
-    constexpr bool COORDS = KIND == IDW_TEMPERATURE && (BYEQ || !SHYFT_IDW_DZREG);
+    constexpr bool COORDS = KIND == IDW_TEMPERATURE && (BYEQ || !DZREG);
     double* sxyz = smem;
     double* tile = smem + (COORDS ? 3 * S : 0);
     if (LDS && COORDS) {
@@ -140,17 +135,17 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
     const double dst_z = KIND == IDW_TEMPERATURE ? a.dst_xyz[3 * (size_t)j + 2] : 0.0;
     int nidx[KT];
     double nw[KT];
-    // naux: precipitation pow(scale, dz/100); temperature (SHYFT_IDW_DZREG) d.z - s.z of each neighbour, the
+    // naux: precipitation pow(scale, dz/100); temperature (DZREG) d.z - s.z of each neighbour, the
     // neighbour table's aux (the same subtraction of the same coordinates), held in registers instead of the
     // per-row LDS read of s.z: K fewer LDS reads per cell-row (not with gradient_by_equation, whose instance has
     // no VGPRs left for it at 2 waves per SIMD)
-    double naux[KIND == IDW_PRECIPITATION || (KIND == IDW_TEMPERATURE && SHYFT_IDW_DZREG && !BYEQ) ? KT : 1];
+    double naux[KIND == IDW_PRECIPITATION || (KIND == IDW_TEMPERATURE && DZREG && !BYEQ) ? KT : 1];
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
         const bool in = k < kept;
         nidx[k] = in ? a.idx[k * N + j] : 0;
         nw[k] = in ? a.w[k * N + j] : 0.0;
-        if (KIND == IDW_PRECIPITATION || (KIND == IDW_TEMPERATURE && SHYFT_IDW_DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
+        if (KIND == IDW_PRECIPITATION || (KIND == IDW_TEMPERATURE && DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
     }
     double* __restrict__ out = a.out;
     // Temperature fast path: when every source value of a row is finite (the common case) the gradient
@@ -333,7 +328,7 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
                     if (k >= kept) continue;
                     const double v = rowp[nidx[k]];
                     double tr;
-                    if (KIND == IDW_TEMPERATURE) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - src_z(nidx[k]));
+                    if (KIND == IDW_TEMPERATURE) tr = v + scale * (DZREG && !BYEQ ? naux[k] : dst_z - src_z(nidx[k]));
                     else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
                     else if (KIND == IDW_RADIATION) tr = v * slope;
                     else tr = v;
@@ -348,7 +343,7 @@ __device__ inline void idw_gather_body(const idw_gather_args& a, int j, bool lan
                 const double v = rowp[nidx[k]];
                 if (!__builtin_isfinite(v)) continue;
                 double tr;
-                if (KIND == IDW_TEMPERATURE) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - src_z(nidx[k]));
+                if (KIND == IDW_TEMPERATURE) tr = v + scale * (DZREG && !BYEQ ? naux[k] : dst_z - src_z(nidx[k]));
                 else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
                 else if (KIND == IDW_RADIATION) tr = v * slope;
                 else tr = v;
@@ -429,11 +424,8 @@ __global__ __launch_bounds__(64) void idw_wave_union_kernel(idw_union_args a) {
     }
 }
 
-#ifndef SHYFT_IDW_WAVE_OCC
-#define SHYFT_IDW_WAVE_OCC 1
-#endif
 template <int KT, int KIND, bool BYEQ>
-__global__ __launch_bounds__(256, SHYFT_IDW_WAVE_OCC) void idw_wave_gather_kernel(idw_gather_args a) {
+__global__ __launch_bounds__(256) void idw_wave_gather_kernel(idw_gather_args a) {
     constexpr int P = 4;  // source rows in flight per lane
     constexpr bool TEMP = KIND == IDW_TEMPERATURE;
     __shared__ double vslot[4][2][64];                 // each wavefront's union values of a row (double-buffered)
@@ -463,12 +455,12 @@ __global__ __launch_bounds__(256, SHYFT_IDW_WAVE_OCC) void idw_wave_gather_kerne
     for (int q = 0; q < (KT + 3) / 4; ++q) lw[q] = 4 * q < kept ? a.lidx[(size_t)q * N + j] : 0u;
     auto L = [&](int k) { return (int)((lw[k >> 2] >> (8 * (k & 3))) & 0xffu); };
     double nw[KT];
-    double naux[KIND == IDW_PRECIPITATION || (TEMP && SHYFT_IDW_DZREG && !BYEQ) ? KT : 1];
+    double naux[KIND == IDW_PRECIPITATION || (TEMP && DZREG && !BYEQ) ? KT : 1];
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
         const bool in = k < kept;
         nw[k] = in ? a.w[k * N + j] : 0.0;
-        if (KIND == IDW_PRECIPITATION || (TEMP && SHYFT_IDW_DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
+        if (KIND == IDW_PRECIPITATION || (TEMP && DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
     }
     const double* zs = zslot[TEMP ? wv : 0];
     const double* xs = xslot[BYEQ ? wv : 0];
@@ -623,7 +615,7 @@ __global__ __launch_bounds__(256, SHYFT_IDW_WAVE_OCC) void idw_wave_gather_kerne
                 const int l = L(k);
                 const double v = row[l];
                 double tr;
-                if (TEMP) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
+                if (TEMP) tr = v + scale * (DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
                 else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
                 else if (KIND == IDW_RADIATION) tr = v * slope;
                 else tr = v;
@@ -640,7 +632,7 @@ __global__ __launch_bounds__(256, SHYFT_IDW_WAVE_OCC) void idw_wave_gather_kerne
                 const int l = L(k) & 63;
                 const double v = row[l];
                 double tr;
-                if (TEMP) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
+                if (TEMP) tr = v + scale * (DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
                 else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
                 else if (KIND == IDW_RADIATION) tr = v * slope;
                 else tr = v;
@@ -656,7 +648,7 @@ __global__ __launch_bounds__(256, SHYFT_IDW_WAVE_OCC) void idw_wave_gather_kerne
             const double v = row[L(k)];
             if (!__builtin_isfinite(v)) continue;
             double tr;
-            if (TEMP) tr = v + scale * (SHYFT_IDW_DZREG && !BYEQ ? naux[k] : dst_z - zs[L(k)]);
+            if (TEMP) tr = v + scale * (DZREG && !BYEQ ? naux[k] : dst_z - zs[L(k)]);
             else if (KIND == IDW_PRECIPITATION) tr = v * naux[k];
             else if (KIND == IDW_RADIATION) tr = v * slope;
             else tr = v;
@@ -689,15 +681,15 @@ hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
     const dim3 grid((a.n_cells + 255) / 256), block(256);
     // LDS: the source coordinates (temperature) + a tile of source rows, up to 32 KB per workgroup
     // (the kernels run at 2 waves per SIMD, 2 workgroups per CU: 60 KB each fits the 160 KB)
-    constexpr size_t LDS_BUDGET = SHYFT_IDW_LDS_KB * 1024;
+    constexpr size_t LDS_BUDGET = LDS_KB * 1024;
     const size_t row_bytes = (size_t)a.n_sources * sizeof(double);
-    const size_t coord_bytes = a.kind == IDW_TEMPERATURE && (a.by_equation || !SHYFT_IDW_DZREG) ? 3 * row_bytes : 0;
+    const size_t coord_bytes = a.kind == IDW_TEMPERATURE && (a.by_equation || !DZREG) ? 3 * row_bytes : 0;
     int lds_rows = row_bytes + coord_bytes <= LDS_BUDGET ? (int)((LDS_BUDGET - coord_bytes) / row_bytes) : 0;
     if (lds_rows > 64) lds_rows = 64;  // row_finite[] flags per tile
     if (lds_rows > a.n_rows) lds_rows = a.n_rows;
     const size_t shm = lds_rows > 0 ? coord_bytes + (size_t)lds_rows * row_bytes : 0;
     // smallest register-resident list that holds max_members, per model
-#define SHYFT_IDW_LAUNCH(KIND_, BYEQ_)                                                                               \
+#define IDW_LAUNCH(KIND_, BYEQ_)                                                                               \
     do {                                                                                                             \
         if (a.max_members <= 8)                                                                                      \
             hipLaunchKernelGGL((idw_gather_kernel<8, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);         \
@@ -708,10 +700,10 @@ hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
         else                                                                                                         \
             hipLaunchKernelGGL((idw_gather_kernel<IDW_KMAX, KIND_, BYEQ_>), grid, block, shm, stream, a, lds_rows);  \
     } while (0)
-#if SHYFT_IDW_WAVE
+    // gathers through the wavefront's union of neighbour stations when every wavefront's union fits 64
     if (a.wu && a.wn && a.lidx) {
         const dim3 wgrid((a.n_cells + 255) / 256);
-#define SHYFT_IDW_WLAUNCH(KIND_, BYEQ_)                                                                              \
+#define IDW_WLAUNCH(KIND_, BYEQ_)                                                                              \
     do {                                                                                                             \
         if (a.max_members <= 8)                                                                                      \
             hipLaunchKernelGGL((idw_wave_gather_kernel<8, KIND_, BYEQ_>), wgrid, block, 0, stream, a);               \
@@ -724,27 +716,26 @@ hipError_t launch_idw_gather(const idw_gather_args& a, hipStream_t stream) {
     } while (0)
         switch (a.kind) {
             case IDW_TEMPERATURE:
-                if (a.by_equation) SHYFT_IDW_WLAUNCH(IDW_TEMPERATURE, true);
-                else SHYFT_IDW_WLAUNCH(IDW_TEMPERATURE, false);
+                if (a.by_equation) IDW_WLAUNCH(IDW_TEMPERATURE, true);
+                else IDW_WLAUNCH(IDW_TEMPERATURE, false);
                 break;
-            case IDW_PRECIPITATION: SHYFT_IDW_WLAUNCH(IDW_PRECIPITATION, false); break;
-            case IDW_RADIATION: SHYFT_IDW_WLAUNCH(IDW_RADIATION, false); break;
-            default: SHYFT_IDW_WLAUNCH(IDW_WIND_SPEED, false); break;
+            case IDW_PRECIPITATION: IDW_WLAUNCH(IDW_PRECIPITATION, false); break;
+            case IDW_RADIATION: IDW_WLAUNCH(IDW_RADIATION, false); break;
+            default: IDW_WLAUNCH(IDW_WIND_SPEED, false); break;
         }
-#undef SHYFT_IDW_WLAUNCH
+#undef IDW_WLAUNCH
         return hipGetLastError();
     }
-#endif
     switch (a.kind) {
         case IDW_TEMPERATURE:
-            if (a.by_equation) SHYFT_IDW_LAUNCH(IDW_TEMPERATURE, true);
-            else SHYFT_IDW_LAUNCH(IDW_TEMPERATURE, false);
+            if (a.by_equation) IDW_LAUNCH(IDW_TEMPERATURE, true);
+            else IDW_LAUNCH(IDW_TEMPERATURE, false);
             break;
-        case IDW_PRECIPITATION: SHYFT_IDW_LAUNCH(IDW_PRECIPITATION, false); break;
-        case IDW_RADIATION: SHYFT_IDW_LAUNCH(IDW_RADIATION, false); break;
-        default: SHYFT_IDW_LAUNCH(IDW_WIND_SPEED, false); break;  // wind speed and rel_hum: plain mean
+        case IDW_PRECIPITATION: IDW_LAUNCH(IDW_PRECIPITATION, false); break;
+        case IDW_RADIATION: IDW_LAUNCH(IDW_RADIATION, false); break;
+        default: IDW_LAUNCH(IDW_WIND_SPEED, false); break;  // wind speed and rel_hum: plain mean
     }
-#undef SHYFT_IDW_LAUNCH
+#undef IDW_LAUNCH
     return hipGetLastError();
 }
 

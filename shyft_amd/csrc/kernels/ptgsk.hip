@@ -24,20 +24,9 @@
 
 using namespace shyft_dev;
 
-// the Brent job of the solving wavefront: gs_corr_lwc_lean (device/gs_brent.h, the same arithmetic in fewer
-// instructions) or the reference-shaped gs_corr_lwc
-#ifndef SHYFT_BRENT_LEAN
-#define SHYFT_BRENT_LEAN 1
-#endif
-// Priestley-Taylor's saturation-pressure exp and actual_evapotranspiration's exp in one dexp2 call
-#ifndef SHYFT_PT_AE2
-#define SHYFT_PT_AE2 1
-#endif
-#if SHYFT_BRENT_LEAN
+// the Brent job of the solving wavefront: gs_corr_lwc_lean (device/gs_brent.h), the arithmetic of the
+// reference-shaped gs_corr_lwc (device/ptgsk_dev.h) in fewer instructions
 #define GS_BRENT_JOB gs_corr_lwc_lean
-#else
-#define GS_BRENT_JOB gs_corr_lwc
-#endif
 
 #ifdef SHYFT_PROF
 // phase timing (profiling builds only): per-wavefront s_memtime deltas summed over the launch
@@ -58,30 +47,22 @@ extern "C" int shyft_ptgsk_prof_read(unsigned long long* out) {
 
 namespace {
 
-#ifndef SHYFT_BLOCK
-#define SHYFT_BLOCK 256
-#endif
-constexpr int BLOCK = SHYFT_BLOCK;
+constexpr int BLOCK = 256;
 
 #ifndef SHYFT_LB_WAVES
 #define SHYFT_LB_WAVES 4
 #endif
 
 // issue priority (s_setprio) of the Brent-solving wavefront: 138.2 -> 134.5 ms per chunk (year mean, 1M cells)
-#ifndef SHYFT_BRENT_PRIO
-#define SHYFT_BRENT_PRIO 3
-#endif
+constexpr int BRENT_PRIO = 3;
 
 // UNIFORM: every cell of the launch uses parameter set 0 (the region parameter, no catchment overrides):
 // the parameter row is then wave-uniform and lives in SGPRs (scalar loads), which frees the VGPRs the
 // per-lane copies would take in the register-bound time loop.
 // ENS: a parameter-ensemble launch (lanes = cells x members): forcing is read from the shared column fcol[lane].
-// SHYFT_PTGSK_LDSC: the 11 per-cell constants in LDS (22 KB per workgroup, 38.9 KB with the job queue: 4
-// workgroups = 16 waves per CU still fit the 160 KB) instead of VGPRs live across the Brent phase. Scratch
-// 400 -> 320 B/lane; 124.8 -> 119.1 ms per 1M-cell chunk over the bench year, bit-exact.
-#ifndef SHYFT_PTGSK_LDSC
-#define SHYFT_PTGSK_LDSC 1
-#endif
+// The 11 per-cell constants live in LDS (22 KB per workgroup, 38.9 KB with the job queue: 4 workgroups = 16
+// waves per CU still fit the 160 KB) instead of VGPRs live across the Brent phase. Scratch 400 -> 320 B/lane;
+// 124.8 -> 119.1 ms per 1M-cell chunk over the bench year, bit-exact.
 // WAVES: the occupancy target. 4 waves per SIMD (128 VGPRs, spilling) is the measured best when the launch fills
 // the GPU; a region too small to give every SIMD 4 waves (<= 2 workgroups per CU, e.g. a strong-scaled shard of
 // 131K cells) gets the 2-wave instance instead (256 VGPRs, no spills): it cannot be 4-deep anyway.
@@ -105,7 +86,6 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     gcell.altitude = cc[PC_ALTITUDE * N + lc];
     gcell.cv2 = cc[PC_CV2 * N + lc];
     gcell.inv_cv2 = cc[PC_INV_CV2 * N + lc];
-#if SHYFT_PTGSK_LDSC
     // the cell constants live in LDS, not in VGPRs: each use reloads its lane's slot (the barriers of the
     // step keep the compiler from hoisting the loads), so none of them is live across the Brent phase
     __shared__ double lcc[11][B];
@@ -137,16 +117,6 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         gcell.cv2 = lcc[2][threadIdx.x];               \
         gcell.inv_cv2 = lcc[3][threadIdx.x];           \
     } while (0)
-#else
-    const double glacier_fraction = cc[PC_GLACIER * N + lc];
-    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
-    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
-    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + lc];
-    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + lc];
-    const double cell_area_m2 = cc[PC_AREA * N + lc];
-    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
-#define LOAD_GCELL() ((void)0)
-#endif
 
     const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
 
@@ -266,17 +236,10 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                     }
                 }
 #else
-#ifdef SHYFT_ROTATE2
-                // the solving wavefront rotates with the step and the workgroup (SIMD load balance)
-                const int t = (threadIdx.x + B - 64 * ((i + (int)blockIdx.x) % (B / 64))) % B;
-#else
                 const int t = threadIdx.x;
-#endif
-#if SHYFT_BRENT_PRIO > 0
                 // the solving wavefront is the workgroup's critical path (its other wavefronts wait at the
                 // barrier below): it gets issue priority over the other workgroups' wavefronts on its SIMD
-                if (t < nj) __builtin_amdgcn_s_setprio(SHYFT_BRENT_PRIO);
-#endif
+                if (t < nj) __builtin_amdgcn_s_setprio(BRENT_PRIO);
                 // the speculative opening when the jobs' point lanes fit the solving wavefront: 4 lanes per job
                 // (z1, u1, u2a, u2b: two f rounds saved) or 2 (z1, u1: one round saved)
                 const int L = SPEC ? (4 * nj <= 64 ? 4 : 2 * nj <= 64 ? 2 : 0) : 0;
@@ -301,9 +264,7 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                 } else {
                     for (int j = t; j < nj; j += B) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
                 }
-#if SHYFT_BRENT_PRIO > 0
                 __builtin_amdgcn_s_setprio(0);
-#endif
 #endif
                 __syncthreads();
                 if (slot >= 0) z = jres[slot];
@@ -327,15 +288,11 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         double gm_melt_m3s = 0.0;
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
-#if SHYFT_PT_AE2
+        // Priestley-Taylor's saturation-pressure exp and actual_evapotranspiration's exp in one dexp2 call
         double ae_exp;
         const double pot_evap =
             pt_pot_evap_exp(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum, -q * 3.0 / P[PK_AE_SCALE], ae_exp) * 3600.0;
         const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(gs_sca, glacier_fraction));
-#else
-        const double pot_evap = pt_pot_evap(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum) * 3600.0;
-        const double ae = pot_evap * (1.0 - dexp(-q * 3.0 / P[PK_AE_SCALE])) * (1.0 - smax(gs_sca, glacier_fraction));
-#endif
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         PROF_MARK(4);  // glacier, PT, AE
         double q_avg;
@@ -377,7 +334,6 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     if (err) a.err[cell] = err;
 }
 #undef LOAD_GCELL
-#if SHYFT_PTGSK_LDSC
 #undef glacier_fraction
 #undef snow_storage_fraction
 #undef kirchner_routed_prec
@@ -385,270 +341,13 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
 #undef kirchner_fraction
 #undef cell_area_m2
 #undef glacier_area_m2
-#endif
-
-// ------------------------------------------------------------------ split launch
-// The step of run_pt_gs_k (pt_gs_k.h:361-396) in two kernels over the same time window:
-//  1. ptgsk_snow_kernel: gamma_snow (gs_front, the workgroup's Brent jobs, gs_back) for every step of the window,
-//     handing the step's snow-covered area and snow outflow to
-//  2. ptgsk_flux_kernel: glacier_melt, priestley_taylor, actual_evapotranspiration and kirchner for every step.
-// gamma_snow does not read anything the later methods of a step compute, so the split changes no arithmetic (the
-// hand-over is two doubles per cell-step through HBM, [2][window][cells]). What it changes is the register
-// footprint: the snow kernel holds the snow state and the Brent queue, the flux kernel the kirchner state and the
-// dopri5 stages, each far below the fused step's 128 VGPRs + spills, so each runs at a higher occupancy -- which
-// is what hides the Brent phase's latency (its other waves wait at the workgroup barrier) in winter.
-#ifndef SHYFT_SNOW_WAVES
-#define SHYFT_SNOW_WAVES 6
-#endif
-#ifndef SHYFT_FLUX_WAVES
-#define SHYFT_FLUX_WAVES 6
-#endif
-
-template <bool UNIFORM, bool ENS>
-__global__ __launch_bounds__(BLOCK, SHYFT_SNOW_WAVES) void ptgsk_snow_kernel(const ptgsk_kargs a) {
-    const int cell = blockIdx.x * blockDim.x + threadIdx.x;
-    bool valid = cell < a.n_cells;
-    if (valid && a.active && !a.active[cell]) valid = false;
-    const int lc = valid ? cell : 0;  // out-of-range lanes join the barriers, read cell 0 and store nothing
-    const size_t N = (size_t)a.n_cells;
-    const size_t NF = ENS ? (size_t)a.f_cols : N;
-    const size_t fcl = ENS ? (size_t)a.fcol[lc] : (size_t)lc;
-    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
-    const double* __restrict__ cc = a.cellc;
-    gs_cell gcell;
-    gcell.forest_fraction = cc[PC_FOREST * N + lc];
-    gcell.altitude = cc[PC_ALTITUDE * N + lc];
-    gcell.cv2 = cc[PC_CV2 * N + lc];
-    gcell.inv_cv2 = cc[PC_INV_CV2 * N + lc];
-    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
-    const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
-
-    double* __restrict__ st = a.state;
-    gs_state s;
-    s.albedo = st[PS_ALBEDO * N + lc];
-    s.lwc = st[PS_LWC * N + lc];
-    s.surface_heat = st[PS_SURFACE_HEAT * N + lc];
-    s.alpha = st[PS_ALPHA * N + lc];
-    s.sdc_melt_mean = st[PS_SDC_MELT_MEAN * N + lc];
-    s.acc_melt = st[PS_ACC_MELT * N + lc];
-    s.iso_pot_energy = st[PS_ISO_POT_ENERGY * N + lc];
-    s.temp_swe = st[PS_TEMP_SWE * N + lc];
-    lgamma_cache lgc;
-    gs_carry carry;
-
-    const size_t TW = (size_t)a.win_len;
-    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * NF;
-    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * NF;
-    const double* __restrict__ f_ws = a.forcing + (size_t)FV_WIND_SPEED * TW * NF;
-    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * NF;
-    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * NF;
-    double* __restrict__ R = a.resp;
-    const size_t RS = TW * N;
-    double* __restrict__ H = a.hand;
-    double* __restrict__ SS = a.state_series;
-    const size_t SSS = (TW + 1) * N;
-    const int wed = (int)P[PK_WED];
-    const int64_t snow_lo = (int64_t)((int)(P[PK_WED] * 24) - (int)(P[PK_NWD] * 24)) * 3600000000LL;
-    const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
-
-    __shared__ double jz1[BLOCK], ja1[BLOCK], jb1[BLOCK], ja2[BLOCK], jb2[BLOCK], jq1[BLOCK], jlg2[BLOCK], jres[BLOCK];
-    __shared__ int jcount[2];
-    if (threadIdx.x == 0) jcount[0] = jcount[1] = 0;  // both: the first step may be odd (start_step)
-    __syncthreads();
-
-    auto collect_state = [&](size_t wi) {  // the snow fields of state_collector::collect (state.scale_snow(ssf))
-        SS[1 * SSS + wi * N + cell] = s.albedo;
-        SS[2 * SSS + wi * N + cell] = s.lwc * snow_storage_fraction;
-        SS[3 * SSS + wi * N + cell] = s.surface_heat;
-        SS[4 * SSS + wi * N + cell] = s.alpha;
-        SS[5 * SSS + wi * N + cell] = s.sdc_melt_mean;
-        SS[6 * SSS + wi * N + cell] = s.acc_melt;
-        SS[7 * SSS + wi * N + cell] = s.iso_pot_energy;
-        SS[8 * SSS + wi * N + cell] = s.temp_swe * snow_storage_fraction;
-    };
-
-    const int i_end = a.step0 + a.n_steps;
-    for (int i = a.step0; i < i_end; ++i) {
-        const size_t wi = (size_t)(i - a.win0);
-        const size_t fo = wi * N + lc;
-        const size_t ff = ENS ? wi * NF + fcl : fo;
-        double temp = 0, rad = 0, rel_hum = 0, prec = 0, wind_speed = 0;
-        if (valid) {
-            temp = f_temp[ff];
-            rad = f_rad[ff];
-            rel_hum = f_rh[ff];
-            prec = f_prec[ff] * P[PK_PCORR];
-            wind_speed = f_ws[ff];
-            if (SS) collect_state(wi);
-        }
-        const bool start_melt = a.doy[i] == wed;
-        const int64_t trel = a.t_rel_year_us[i];
-        const bool snow_season = trel >= snow_lo && trel < snow_hi;
-        gs_mid m;
-        m.need = false;
-        m.done = true;
-        if (valid)
-            gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc, carry);
-        double z = 0.0;
-        if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (race-free: see DESIGN.md)
-        int slot = -1;
-        if (m.need) {
-            slot = atomicAdd(&jcount[i & 1], 1);
-            jz1[slot] = m.z1; ja1[slot] = m.a1; jb1[slot] = m.b1; ja2[slot] = m.a2; jb2[slot] = m.b2;
-            jq1[slot] = m.q1; jlg2[slot] = m.lga2;
-        }
-        __syncthreads();
-        const int nj = jcount[i & 1];
-        if (nj > 0) {
-            const int t = threadIdx.x;
-#if SHYFT_BRENT_PRIO > 0
-            if (t < nj) __builtin_amdgcn_s_setprio(SHYFT_BRENT_PRIO);
-#endif
-#ifdef SHYFT_PROF
-            int nf = 0;
-            for (int j = t; j < nj; j += BLOCK) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j], nf);
-#else
-            for (int j = t; j < nj; j += BLOCK) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
-#endif
-#if SHYFT_BRENT_PRIO > 0
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            __syncthreads();
-            if (slot >= 0) z = jres[slot];
-        }
-        if (!valid) continue;
-        double gs_sca, gs_storage, gs_outflow;
-        gs_back(s, m, z, gs_sca, gs_storage, gs_outflow, snow_season, a.dt_us, P, gcell, prec, lgc, carry);
-        H[fo] = gs_sca;
-        H[RS + fo] = gs_outflow;
-        if (a.collect >= 1) {
-            R[PR_SNOW_SCA * RS + fo] = gs_sca;
-            R[PR_SNOW_SWE * RS + fo] = gs_storage * snow_storage_fraction;
-        }
-        if (a.collect >= 2)
-            R[PR_SNOW_OUTFLOW * RS + fo] = cc[PC_AREA * N + lc] * (gs_outflow * snow_storage_fraction) * mmh_to_m3s_scale_factor;
-        if (SS && i + 1 == i_end) collect_state(wi + 1);
-    }
-    if (!valid) return;
-    st[PS_ALBEDO * N + cell] = s.albedo;
-    st[PS_LWC * N + cell] = s.lwc;
-    st[PS_SURFACE_HEAT * N + cell] = s.surface_heat;
-    st[PS_ALPHA * N + cell] = s.alpha;
-    st[PS_SDC_MELT_MEAN * N + cell] = s.sdc_melt_mean;
-    st[PS_ACC_MELT * N + cell] = s.acc_melt;
-    st[PS_ISO_POT_ENERGY * N + cell] = s.iso_pot_energy;
-    st[PS_TEMP_SWE * N + cell] = s.temp_swe;
-}
-
-template <bool UNIFORM, bool ENS>
-__global__ __launch_bounds__(BLOCK, SHYFT_FLUX_WAVES) void ptgsk_flux_kernel(const ptgsk_kargs a) {
-    const int cell = blockIdx.x * blockDim.x + threadIdx.x;
-    if (cell >= a.n_cells) return;
-    if (a.active && !a.active[cell]) return;
-    const size_t N = (size_t)a.n_cells;
-    const size_t NF = ENS ? (size_t)a.f_cols : N;
-    const size_t fcl = ENS ? (size_t)a.fcol[cell] : (size_t)cell;
-    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * PTGSK_NP;
-    const double* __restrict__ cc = a.cellc;
-    const double glacier_fraction = cc[PC_GLACIER * N + cell];
-    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + cell];
-    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + cell];
-    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + cell];
-    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + cell];
-    const double cell_area_m2 = cc[PC_AREA * N + cell];
-    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + cell];
-    const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
-    double* __restrict__ st = a.state;
-    double q = st[PS_KIRCHNER_Q * N + cell];
-    int32_t err = 0;
-
-    const size_t TW = (size_t)a.win_len;
-    const double* __restrict__ f_temp = a.forcing + (size_t)FV_TEMPERATURE * TW * NF;
-    const double* __restrict__ f_prec = a.forcing + (size_t)FV_PRECIPITATION * TW * NF;
-    const double* __restrict__ f_rh = a.forcing + (size_t)FV_REL_HUM * TW * NF;
-    const double* __restrict__ f_rad = a.forcing + (size_t)FV_RADIATION * TW * NF;
-    double* __restrict__ R = a.resp;
-    const size_t RS = TW * N;
-    const double* __restrict__ H = a.hand;
-    double* __restrict__ SS = a.state_series;
-
-    const int i_end = a.step0 + a.n_steps;
-    for (int i = a.step0; i < i_end; ++i) {
-        const double gm_direct = P[PK_GM_DIRECT];
-        const double gm_routed = 1 - gm_direct;
-        const size_t wi = (size_t)(i - a.win0);
-        const size_t fo = wi * N + cell;
-        const size_t ff = ENS ? wi * NF + fcl : fo;
-        const double temp = f_temp[ff];
-        const double rad = f_rad[ff];
-        const double rel_hum = f_rh[ff];
-        const double prec = f_prec[ff] * P[PK_PCORR];
-        const double gs_sca = H[fo];
-        const double gs_outflow = H[RS + fo];
-        if (SS) SS[wi * N + cell] = cell_area_m2 * q * mmh_to_m3s_scale_factor;
-        // glacier_melt::step (glacier_melt.h:47-52)
-        const double sca_area = cell_area_m2 * gs_sca;
-        double gm_melt_m3s = 0.0;
-        if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
-            gm_melt_m3s = P[PK_DTF] * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
-#if SHYFT_PT_AE2
-        double ae_exp;
-        const double pot_evap =
-            pt_pot_evap_exp(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum, -q * 3.0 / P[PK_AE_SCALE], ae_exp) * 3600.0;
-        const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(gs_sca, glacier_fraction));
-#else
-        const double pot_evap = pt_pot_evap(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum) * 3600.0;
-        const double ae = pot_evap * (1.0 - dexp(-q * 3.0 / P[PK_AE_SCALE])) * (1.0 - smax(gs_sca, glacier_fraction));
-#endif
-        const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
-        double q_avg;
-        if (!kirchner_step(q, q_avg, gs_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
-                           ae, a.t1_hours, P[PK_C1], P[PK_C2], P[PK_C3]))
-            err = ERR_KIRCHNER_MAX_ITER;
-        const double total_discharge = smax(0.0, prec - ae) * direct_response_fraction + gm_direct * gm_mmh +
-                                       q_avg * kirchner_fraction;
-        const double charge_m3s = +(cell_area_m2 * prec * mmh_to_m3s_scale_factor) -
-                                  (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
-                                  (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
-        R[PR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
-        R[PR_CHARGE_M3S * RS + fo] = charge_m3s;
-        if (a.collect >= 2) {
-            R[PR_GLACIER_MELT * RS + fo] = gm_melt_m3s;
-            R[PR_AE_OUTPUT * RS + fo] = ae;
-            R[PR_PE_OUTPUT * RS + fo] = pot_evap;
-        }
-        if (SS && i + 1 == i_end) SS[(wi + 1) * N + cell] = cell_area_m2 * q * mmh_to_m3s_scale_factor;
-    }
-    st[PS_KIRCHNER_Q * N + cell] = q;
-    if (err) a.err[cell] = err;
-}
 
 }  // namespace
 
 
-#ifndef SHYFT_COMPACT_DEFAULT
-#define SHYFT_COMPACT_DEFAULT 1
-#endif
-
-hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t ev_mid) {
+hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (SHYFT_PTGSK_SPLIT && a.hand) {
-        if (a.fcol) hipLaunchKernelGGL((ptgsk_snow_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else if (a.uniform_params) hipLaunchKernelGGL((ptgsk_snow_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else hipLaunchKernelGGL((ptgsk_snow_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if (ev_mid && (e = hipEventRecord(ev_mid, stream)) != hipSuccess) return e;
-        if (a.fcol) hipLaunchKernelGGL((ptgsk_flux_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else if (a.uniform_params) hipLaunchKernelGGL((ptgsk_flux_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else hipLaunchKernelGGL((ptgsk_flux_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        return hipGetLastError();
-    }
-    if (ev_mid) {
-        hipError_t e = hipEventRecord(ev_mid, stream);
-        if (e != hipSuccess) return e;
-    }
     // workgroups resident at 4 waves per SIMD: 4 per CU (16 waves of 256-lane workgroups)
     int n_cu = 256;
     {
@@ -660,30 +359,19 @@ hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream, hipEvent_t
     }
     static const char* force = getenv("SHYFT_PTGSK_WAVES");  // measurement knob: "2" / "4" forces an instance
     const bool small = force ? force[0] == '2' : grid <= 2 * n_cu;
-    if (a.fcol)
+    if (a.fcol) {
         hipLaunchKernelGGL((ptgsk_run_kernel<true, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (SHYFT_COMPACT_DEFAULT && small) {
+    } else if (small) {
         // small regions: one-wavefront workgroups (each wavefront solves its own ~7 winter Brent jobs: no workgroup
         // barrier wait) with the speculative Brent opening (4 lanes per job, free in a wavefront that has the lanes)
-        static const char* sm = getenv("SHYFT_PTGSK_SMALL");  // measurement knob: "256" = the 256-lane instance,
-        const int smode = sm ? atoi(sm) : 64;                 // "65" = 64 lanes without the speculation
         const int g64 = (a.n_cells + 63) / 64;
-        if (smode == 256) {
-            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
-            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        } else if (smode == 65) {
-            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2, 64, false>), dim3(g64), dim3(64), 0, stream, a);
-            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2, 64, false>), dim3(g64), dim3(64), 0, stream, a);
-        } else {
-            if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
-            else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
-        }
-    } else if (SHYFT_COMPACT_DEFAULT) {
+        if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
+        else hipLaunchKernelGGL((ptgsk_run_kernel<true, false, false, 2, 64, true>), dim3(g64), dim3(64), 0, stream, a);
+    } else {
         // (the speculative Brent opening in this instance measured 100.5 -> 134.7 ms per 1M-cell chunk, year mean:
         // its memo registers spill in every phase of the 128-VGPR step loop, so it stays a small-region feature)
         if (a.uniform_params) hipLaunchKernelGGL((ptgsk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
         else hipLaunchKernelGGL((ptgsk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    } else
-        hipLaunchKernelGGL((ptgsk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    }
     return hipGetLastError();
 }

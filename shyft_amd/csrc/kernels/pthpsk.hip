@@ -24,19 +24,17 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTHPSK_WAVES=N, 0 = the compiler's choice)
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTHPSK_WAVES=N): per-lane parameter rows
 #ifndef SHYFT_PTHPSK_WAVES
 #define SHYFT_PTHPSK_WAVES 2  // measured: compiler choice (1) 151 ms, 2: 91, 3: 123
 #endif
-#ifndef SHYFT_PTHPSK_WAVES_U
-#define SHYFT_PTHPSK_WAVES_U 3  // the uniform-parameter instance; measured: 2: 93.4, 3: 85.0 ms per chunk (per-lane rows at 2: 91.0)
-#endif
-#define SHYFT_PTHPSK_W (UNIFORM ? SHYFT_PTHPSK_WAVES_U : SHYFT_PTHPSK_WAVES)
-#define SHYFT_PTHPSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHPSK_W, SHYFT_PTHPSK_W)))
+constexpr int WAVES_UNIFORM = 3;  // the uniform-parameter instance; measured: 2: 93.4, 3: 85.0 ms per chunk (per-lane rows at 2: 91.0)
 
 // UNIFORM: every cell uses parameter set 0 (the parameter row wave-uniform, in SGPRs instead of VGPRs)
 template <bool UNIFORM>
-__global__ __launch_bounds__(BLOCK) SHYFT_PTHPSK_OCC void pthpsk_run_kernel(const pthpsk_kargs a) {
+__global__ __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(UNIFORM ? WAVES_UNIFORM : SHYFT_PTHPSK_WAVES, UNIFORM ? WAVES_UNIFORM : SHYFT_PTHPSK_WAVES)))
+void pthpsk_run_kernel(const pthpsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;

@@ -24,21 +24,19 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTHSK_WAVES=N, 0 = the compiler's choice)
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTHSK_WAVES=N): per-lane parameter rows
 #ifndef SHYFT_PTHSK_WAVES
 #define SHYFT_PTHSK_WAVES 3  // measured: compiler choice (1) 123 ms, 2: 70, 3: 64, 4: 70 per 730-step chunk
 #endif
-#ifndef SHYFT_PTHSK_WAVES_U
-#define SHYFT_PTHSK_WAVES_U 4  // the uniform-parameter instance; measured (5 bins): 2: 69.2, 3: 55.3, 4: 50.6 ms per chunk
-#endif
-#define SHYFT_PTHSK_W (UNIFORM ? SHYFT_PTHSK_WAVES_U : SHYFT_PTHSK_WAVES)
-#define SHYFT_PTHSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTHSK_W, SHYFT_PTHSK_W)))
+constexpr int WAVES_UNIFORM = 4;  // the uniform-parameter instance; measured (5 bins): 2: 69.2, 3: 55.3, 4: 50.6 ms per chunk
 
 // UNIFORM: every cell uses parameter set 0 (the row, incl. the bin distribution, in SGPRs instead of VGPRs).
 // NB: register capacity of the snow bins, HBV_MAX_BINS or 5 (as in the hbv_stack kernel: one parameter set of at
 // most 5 bins and no state series; bins NB..7 of the state are written as 0, the oracle's padding).
 template <bool UNIFORM, int NB>
-__global__ __launch_bounds__(BLOCK) SHYFT_PTHSK_OCC void pthsk_run_kernel(const pthsk_kargs a) {
+__global__ __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(UNIFORM ? WAVES_UNIFORM : SHYFT_PTHSK_WAVES, UNIFORM ? WAVES_UNIFORM : SHYFT_PTHSK_WAVES)))
+void pthsk_run_kernel(const pthsk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     if (cell >= a.n_cells) return;
     if (a.active && !a.active[cell]) return;

@@ -23,14 +23,9 @@ namespace {
 
 constexpr int BLOCK = 256;
 
-// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTSSK_WAVES=N, 0 = the compiler's choice)
+// occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTSSK_WAVES=N)
 #ifndef SHYFT_PTSSK_WAVES
 #define SHYFT_PTSSK_WAVES 4  // measured: compiler choice (2) 188 ms, 3: 153, 4: 145, 5: 143, 6: 142
-#endif
-#if SHYFT_PTSSK_WAVES > 0
-#define SHYFT_PTSSK_OCC __attribute__((amdgpu_waves_per_eu(SHYFT_PTSSK_WAVES, SHYFT_PTSSK_WAVES)))
-#else
-#define SHYFT_PTSSK_OCC
 #endif
 
 // sca_rel_red compaction (COMPACT): a partial melt calls statistics::sca_rel_red (skaugen.h:57-82: a 2-bit
@@ -38,23 +33,17 @@ constexpr int BLOCK = 256;
 // step, scattered over the wavefronts. Each step the workgroup queues its lanes' calls in LDS and the first
 // ceil(jobs/64) wavefronts evaluate them, one per lane; every lane then finishes its step with its own result
 // (the same function of the same arguments: bit-identical to the per-lane call).
-#ifndef SHYFT_PTSSK_COMPACT
-#define SHYFT_PTSSK_COMPACT 1
-#endif
-#ifndef SHYFT_PTSSK_PRIO
-#define SHYFT_PTSSK_PRIO 3  // measured: 135.3 -> 134.5 ms per chunk
-#endif
+// The solving wavefronts run at issue priority 3 (measured: 135.3 -> 134.5 ms per chunk).
+constexpr int JOB_PRIO = 3;
 
-// SHYFT_PTSSK_LDSC: the 7 per-cell constants in LDS (14 KB per workgroup next to the 11 KB job queue) instead
-// of VGPRs live across the sca_rel_red phase (as in the pt_gs_k kernel).
-#ifndef SHYFT_PTSSK_LDSC
-#define SHYFT_PTSSK_LDSC 1
-#endif
+// The 7 per-cell constants live in LDS (14 KB per workgroup next to the 11 KB job queue) instead of VGPRs live
+// across the sca_rel_red phase (as in the pt_gs_k kernel).
 
 // UNIFORM: every cell uses parameter set 0, so the parameter row is wave-uniform (SGPRs, not 18 per-lane
 // doubles held in VGPRs for the whole launch)
 template <bool COMPACT, bool UNIFORM>
-__global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const ptssk_kargs a) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SHYFT_PTSSK_WAVES, SHYFT_PTSSK_WAVES)))
+void ptssk_run_kernel(const ptssk_kargs a) {
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
     if (valid && a.active && !a.active[cell]) valid = false;
@@ -90,7 +79,6 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     const double gm_routed = 1 - gm_direct;
 
     const double* __restrict__ cc = a.cellc;  // pt_ss_k.h:237-245 (same rows as pt_gs_k)
-#if SHYFT_PTSSK_LDSC
     __shared__ double lcc[7][BLOCK];
     {
         const int t = threadIdx.x;
@@ -109,15 +97,6 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
 #define kirchner_fraction (lcc[4][threadIdx.x])
 #define cell_area_m2 (lcc[5][threadIdx.x])
 #define glacier_area_m2 (lcc[6][threadIdx.x])
-#else
-    const double glacier_fraction = cc[PC_GLACIER * N + lc];
-    const double snow_storage_fraction = cc[PC_SNOW_STORAGE * N + lc];
-    const double kirchner_routed_prec = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
-    const double direct_response_fraction = cc[PC_DIRECT_RESPONSE * N + lc];
-    const double kirchner_fraction = cc[PC_KIRCHNER_FRACTION * N + lc];
-    const double cell_area_m2 = cc[PC_AREA * N + lc];
-    const double glacier_area_m2 = cc[PC_GLACIER_AREA * N + lc];
-#endif
     const double mmh_to_m3s_scale_factor = 1 / (3600.0 * 1000.0);
 
     double* __restrict__ st = a.state;
@@ -182,17 +161,13 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
             __syncthreads();
             const int nj = jcount[i & 1];
             if (nj > 0) {
-#if SHYFT_PTSSK_PRIO > 0
-                if ((int)threadIdx.x < nj) __builtin_amdgcn_s_setprio(SHYFT_PTSSK_PRIO);  // the workgroup's critical path
-#endif
+                if ((int)threadIdx.x < nj) __builtin_amdgcn_s_setprio(JOB_PRIO);  // the workgroup's critical path
                 for (int j = threadIdx.x; j < nj; j += BLOCK) {
                     int32_t e = 0;
                     jres[j] = ss_sca_rel_red(ju[j], jn[j], jnu[j], jal[j], e);
                     jerr[j] = e;
                 }
-#if SHYFT_PTSSK_PRIO > 0
                 __builtin_amdgcn_s_setprio(0);
-#endif
                 __syncthreads();
                 if (slot >= 0) {
                     rel = jres[slot];
@@ -248,7 +223,6 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
     st[SS_KIRCHNER_Q * N + cell] = q;
     if (err) a.err[cell] = err;
 }
-#if SHYFT_PTSSK_LDSC
 #undef glacier_fraction
 #undef snow_storage_fraction
 #undef kirchner_routed_prec
@@ -256,15 +230,13 @@ __global__ __launch_bounds__(BLOCK) SHYFT_PTSSK_OCC void ptssk_run_kernel(const 
 #undef kirchner_fraction
 #undef cell_area_m2
 #undef glacier_area_m2
-#endif
 
 }  // namespace
 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (!SHYFT_PTSSK_COMPACT) hipLaunchKernelGGL((ptssk_run_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (a.uniform_params) hipLaunchKernelGGL((ptssk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (a.uniform_params) hipLaunchKernelGGL((ptssk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else hipLaunchKernelGGL((ptssk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();
 }

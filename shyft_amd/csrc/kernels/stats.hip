@@ -155,3 +155,39 @@ hipError_t launch_nan_scan(const double* f, size_t n_rows, size_t n_cells, const
     hipLaunchKernelGGL(nan_scan_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, f, n_rows, n_cells, active, flag);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------- sharded regions (shards.hip)
+namespace {
+// dst[rows[r]][t] = src[r][t]: a shard's partial sums into the region's row order
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const double* __restrict__ src, const int32_t* __restrict__ rows,
+                                                           size_t n_rows, size_t n, double* __restrict__ dst) {
+    const size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n_rows * n) return;
+    const size_t r = i / n, t = i - r * n;
+    dst[size_t(rows[r]) * n + t] = src[i];
+}
+// out[j] = ((g[0][j] + g[1][j]) + g[2][j]) + ...: the shards' partials added in shard order (deterministic)
+__global__ __launch_bounds__(256) void ordered_sum_kernel(const double* __restrict__ g, size_t S, size_t M,
+                                                          double* __restrict__ out) {
+    const size_t j = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (j >= M) return;
+    double v = g[j];
+    for (size_t k = 1; k < S; ++k) v += g[k * M + j];
+    out[j] = v;
+}
+}  // namespace
+
+hipError_t launch_scatter_rows(const double* src, const int32_t* rows, size_t n_rows, size_t n, double* dst,
+                               hipStream_t stream) {
+    const size_t m = n_rows * n;
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3(unsigned((m + 255) / 256)), dim3(256), 0, stream, src, rows, n_rows, n,
+                       dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_ordered_sum(const double* g, size_t S, size_t M, double* out, hipStream_t stream) {
+    if (M == 0) return hipSuccess;
+    hipLaunchKernelGGL(ordered_sum_kernel, dim3(unsigned((M + 255) / 256)), dim3(256), 0, stream, g, S, M, out);
+    return hipGetLastError();
+}

@@ -20,42 +20,23 @@
 #include "../../include/shyft_hip.h"
 #include "include_internal/kernels.h"
 #include "include_internal/layout.h"
+#include "include_internal/region_impl.h"
+#include "include_internal/shards.h"
 #include "include_internal/synth_hash.h"
 #include "../../detmath/detmath.h"
 
-namespace {
-
+namespace shyft_hip_impl {
 thread_local std::string g_last_error;
-
-struct hip_error : std::runtime_error {
-    using std::runtime_error::runtime_error;
-};
-
-void hip_check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw hip_error(std::string(what) + ": " + hipGetErrorString(e));
+int fail(shyft_hip_region* h, const std::string& msg) {
+    if (h) h->err = msg;
+    g_last_error = msg;
+    return 1;
 }
+}  // namespace shyft_hip_impl
 
-template <class T>
-struct dbuf {
-    T* p = nullptr;
-    size_t n = 0;
-    dbuf() = default;
-    dbuf(const dbuf&) = delete;
-    dbuf& operator=(const dbuf&) = delete;
-    ~dbuf() { release(); }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-    }
-    void alloc(size_t count) {
-        if (count == n && p) return;
-        release();
-        if (count == 0) return;
-        hip_check(hipMalloc(&p, count * sizeof(T)), "hipMalloc");
-        n = count;
-    }
-};
+using namespace shyft_hip_impl;
+
+namespace {
 
 // UTC civil calendar (core/utctime_utilities.cpp:230-253)
 int64_t floor_div(int64_t a, int64_t b) {
@@ -103,119 +84,9 @@ double btk_prior_gradient(int64_t start_us, int64_t dt_us) {
 
 }  // namespace
 
-struct shyft_hip_region {
-    int stack = 0;
-    size_t n = 0;
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;  // ev_mid: between the split pt_gs_k kernels
-    hipEvent_t ev_copy = nullptr;  // shyft_hip_copy_state: the copy out of this region's state has finished
-    std::string err;
-    double last_ms = 0.0;
-    double last_part_ms[2] = {0.0, 0.0};  // pt_gs_k: snow kernel, flux kernel (split launch)
-    int last_parts = 1;
-
-    // host mirrors
-    std::vector<double> geo;  // n x 11
-    std::vector<int64_t> routing_id;
-    std::vector<double> routing_distance;
-    std::vector<int64_t> cid;          // per cell
-    std::vector<size_t> cix;           // per cell
-    std::vector<int64_t> cix_to_cid;   // region_model::cix_to_cid
-    std::map<int64_t, size_t> cid_to_cix;
-    std::vector<double> params;        // n_sets x param_width()
-    size_t n_sets = 0;
-    std::vector<int32_t> set_ix;
-    std::vector<uint8_t> active;       // empty = no filter
-    int64_t t0 = 0, dt = 0;
-    size_t T = 0, w0 = 0, TW = 0;
-    int collect = COLLECT_DISCHARGE;
-    int collect_state = 0;
-    bool derived_dirty = true;
-    bool has_geo = false, has_params = false, has_state = false;
-
-    // device
-    dbuf<double> d_params, d_cellc, d_state, d_forcing, d_resp, d_state_series;
-    dbuf<double> d_hand;  // pt_gs_k: [2][TW][n] gamma_snow -> flux hand-over of the split launch
-    // double-buffered forcing window (shyft_hip_prefetch_synthetic_forcing / shyft_hip_swap_forcing_window): the
-    // next window is generated on gen_stream (restricted to a few CUs) while the current one runs
-    dbuf<double> d_forcing_next;
-    hipStream_t gen_stream = nullptr;
-    int gen_cus = -1;
-    hipEvent_t ev_gen = nullptr;
-    size_t gen_w0 = SIZE_MAX;
-    dbuf<int32_t> d_set_ix, d_err, d_doy, d_seg_cells, d_seg_off, d_sel;
-    dbuf<int64_t> d_trel;
-    dbuf<uint8_t> d_active;
-    dbuf<double> d_tmp, d_w, d_alt;
-    dbuf<int32_t> d_flag;
-
-    // inverse-distance neighbour tables, one per forcing variable, cached by
-    // (model, parameters, source geometry)
-    struct idw_table {
-        std::vector<double> key;
-        dbuf<int32_t> idx, cnt;
-        dbuf<double> w, aux;
-        dbuf<int32_t> wu, wn, ovf;  // wavefront unions of the neighbour lists (idw_wave_union)
-        dbuf<uint32_t> lidx;
-        bool wave_ok = false;
-        int K = 0;
-        int last_path = SHYFT_HIP_IDW_NONE;  // the gather the last interpolate of this variable ran
-    } idw[N_FORCING];
-    dbuf<double> d_dst_xyz, d_slope, d_src_xyz, d_src_vals;
-    bool dst_dirty = true;
-    // Bayesian temperature kriging destinations (calculated cells) and their window columns
-    dbuf<double> d_btk_xyz;
-    dbuf<int32_t> d_btk_index;
-    std::vector<double> btk_xyz_host;
-    std::vector<int32_t> btk_index_host;
-    uint64_t btk_dst_version = 0;
-    std::unique_ptr<btk_cache, void (*)(btk_cache*)> btk{nullptr, btk_cache_destroy};
-
-    // routing groups (cells sharing river + UHG): segment tables for the group discharge sums
-    dbuf<int32_t> d_rseg_cells, d_rseg_off;
-    size_t n_route_groups = 0;
-
-    // parameter ensemble (calibration): a lane region of calculated cells x members that reads this
-    // region's forcing through d_fcol (see shyft_hip_ensemble_run)
-    shyft_hip_region* ens = nullptr;
-    const shyft_hip_region* forcing_src = nullptr;  // set on an ensemble lane region: whose forcing it reads
-    dbuf<int32_t> d_fcol;                            // [lanes] forcing column (cell of the parent region)
-    size_t ens_members = 0, ens_cells = 0, ens_groups = 0, ens_b = 0, ens_e = 0;
-
-    bool hbv() const { return stack == SHYFT_HIP_HBV_STACK; }
-    bool ptssk() const { return stack == SHYFT_HIP_PT_SS_K; }
-    bool pthsk() const { return stack == SHYFT_HIP_PT_HS_K; }
-    bool pthpsk() const { return stack == SHYFT_HIP_PT_HPS_K; }
-    size_t n_series() const {
-        if (collect == COLLECT_ALL) return hbv() ? HBV_NR : PTGSK_NR;
-        return collect == COLLECT_DISCHARGE_SNOW ? 4 : 2;
-    }
-    size_t n_state_fields() const {
-        return hbv() ? HBV_NS : (ptssk() ? PTSSK_NS : (pthsk() ? PTHSK_NS : (pthpsk() ? PTHPSK_NS : PTGSK_NS)));
-    }
-    // state-collector series per cell (pt_ss_k collects 7 series from its 8 state values)
-    size_t n_state_series() const {
-        return ptssk() ? PTSSK_NSC : (pthsk() ? PTHSK_NSC : (pthpsk() ? PTHPSK_NSC : n_state_fields()));
-    }
-    size_t n_ref_params() const {
-        return hbv() ? HBV_NP_REF
-                     : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP_REF : (pthpsk() ? PTHPSK_NP_REF : PTGSK_NP_REF)));
-    }
-    size_t param_width() const {
-        return hbv() ? HBV_NP : (ptssk() ? PTSSK_NP : (pthsk() ? PTHSK_NP : (pthpsk() ? PTHPSK_NP : PTGSK_NP_REF)));
-    }
-    // hbv_snow quantile distribution (n_bins, s[], intervals[]) in the parameter row, or -1
-    int snow_dist_index() const { return hbv() ? HK_NB : (pthsk() ? PH_NB : (pthpsk() ? PP_NB : -1)); }
-};
 
 namespace {
 
-int fail(shyft_hip_region* h, const std::string& msg) {
-    if (h) h->err = msg;
-    g_last_error = msg;
-    return 1;
-}
 
 // host <-> region copies are ordered on the region's stream (created non-blocking, so a null-stream copy would
 // not wait for a run or copy_state still queued there) and complete before returning, like hipMemcpy
@@ -225,18 +96,6 @@ hipError_t region_copy(shyft_hip_region* h, void* dst, const void* src, size_t b
     return hipStreamSynchronize(h->stream);
 }
 
-template <class F>
-int guarded(shyft_hip_region* h, F&& f) {
-    try {
-        if (h) hip_check(hipSetDevice(h->device), "hipSetDevice");
-        f();
-        return 0;
-    } catch (const std::exception& e) {
-        return fail(h, e.what());
-    } catch (...) {
-        return fail(h, "unknown error");
-    }
-}
 
 // region_model::update_ix_to_id_mapping (region_model.h:236-252)
 void update_ix_to_id_mapping(shyft_hip_region* h) {
@@ -503,7 +362,6 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
         hip_check(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
         hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
         hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
-        hip_check(hipEventCreate(&h->ev_mid), "hipEventCreate");
         hip_check(hipEventCreateWithFlags(&h->ev_copy, hipEventDisableTiming), "hipEventCreate");
         h->d_state.alloc(h->n_state_fields() * n_cells);
         h->d_err.alloc(n_cells);
@@ -517,15 +375,51 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
     return 0;
 }
 
+int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* devices, size_t n_shards,
+                                    shyft_hip_region** out) {
+    if (!out) return fail(nullptr, "shyft_hip_region_create_sharded: out is null");
+    *out = nullptr;
+    if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK && stack != SHYFT_HIP_PT_SS_K &&
+        stack != SHYFT_HIP_PT_HS_K && stack != SHYFT_HIP_PT_HPS_K)
+        return fail(nullptr, "shyft_hip_region_create: unsupported method stack");
+    if (n_cells == 0 || n_cells > (size_t)INT32_MAX) return fail(nullptr, "shyft_hip_region_create: invalid n_cells");
+    try {
+        std::unique_ptr<shyft_hip_region> h(new shyft_hip_region());
+        h->stack = stack;
+        h->n = n_cells;
+        h->device = devices && n_shards ? devices[0] : 0;
+        h->sh = shard_set_create(stack, n_cells, devices, n_shards);
+        *out = h.release();
+        return 0;
+    } catch (const std::exception& e) {
+        return fail(nullptr, e.what());
+    }
+}
+
+size_t shyft_hip_region_shards(const shyft_hip_region* h, size_t k, int* device, size_t* cell0, size_t* n_cells) {
+    if (!h) return 0;
+    if (h->sh) return shards::info(h->sh, k, device, cell0, n_cells);
+    if (k == 0) {
+        if (device) *device = h->device;
+        if (cell0) *cell0 = 0;
+        if (n_cells) *n_cells = h->n;
+    }
+    return 1;
+}
+
+int shyft_hip_region_combine_path(const shyft_hip_region* h) {
+    return h && h->sh ? shards::combine_path(h->sh) : SHYFT_HIP_COMBINE_NONE;
+}
+
 void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (!h) return;
+    if (h->sh) shard_set_destroy(h->sh);
     if (h->ens) shyft_hip_region_destroy(h->ens);
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->gen_stream) (void)hipStreamSynchronize(h->gen_stream);  // a prefetch may still write d_forcing_next
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
-    if (h->ev_mid) (void)hipEventDestroy(h->ev_mid);
     if (h->ev_gen) (void)hipEventDestroy(h->ev_gen);
     if (h->gen_stream) (void)hipStreamDestroy(h->gen_stream);
     if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
@@ -537,6 +431,7 @@ size_t shyft_hip_region_size(const shyft_hip_region* h) { return h ? h->n : 0; }
 
 int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* routing_id, const double* routing_distance) {
     if (!h || !geo11) return fail(h, "shyft_hip_set_geo: null argument");
+    if (h->sh) return guarded(h, [&] { shards::set_geo(h->sh, geo11, routing_id, routing_distance); });
     return guarded(h, [&] {
         for (size_t i = 0; i < h->n; ++i) {
             const double* g = geo11 + i * 11;
@@ -571,6 +466,7 @@ int shyft_hip_set_geo(shyft_hip_region* h, const double* geo11, const int64_t* r
 int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n_sets, size_t n_per_set,
                              const int32_t* set_ix) {
     if (!h || !params) return fail(h, "shyft_hip_set_parameters: null argument");
+    if (h->sh) return guarded(h, [&] { shards::set_parameters(h->sh, params, n_sets, n_per_set, set_ix); });
     return guarded(h, [&] {
         const size_t width = h->param_width();
         if (h->hbv()) {
@@ -627,6 +523,7 @@ int shyft_hip_set_parameters(shyft_hip_region* h, const double* params, size_t n
 
 int shyft_hip_set_time_axis(shyft_hip_region* h, int64_t t0_us, int64_t dt_us, size_t n_steps, size_t window_steps) {
     if (!h) return fail(h, "shyft_hip_set_time_axis: null handle");
+    if (h->sh) return guarded(h, [&] { shards::set_time_axis(h->sh, t0_us, dt_us, n_steps, window_steps); });
     return guarded(h, [&] {
         if (dt_us <= 0 || n_steps == 0) throw std::runtime_error("region_model::run with invalid time_axis invoked");
         if (n_steps > (size_t)INT32_MAX) throw std::runtime_error("time axis too long");
@@ -659,6 +556,7 @@ int shyft_hip_set_window(shyft_hip_region* h, size_t w0) { return shyft_hip_move
 
 int shyft_hip_move_window(shyft_hip_region* h, size_t w0, int fill_mask) {
     if (!h) return fail(h, "shyft_hip_set_window: null handle");
+    if (h->sh) return guarded(h, [&] { shards::move_window(h->sh, w0, fill_mask); });
     return guarded(h, [&] {
         if (h->T == 0) throw std::runtime_error("set_window: no time axis");
         if (w0 + h->TW > h->T) throw std::runtime_error("set_window: window beyond the time axis");
@@ -673,6 +571,7 @@ int shyft_hip_move_window(shyft_hip_region* h, size_t w0, int fill_mask) {
 
 int shyft_hip_set_collection(shyft_hip_region* h, int collect, int collect_state) {
     if (!h) return fail(h, "shyft_hip_set_collection: null handle");
+    if (h->sh) return guarded(h, [&] { shards::set_collection(h->sh, collect, collect_state); });
     return guarded(h, [&] {
         if (collect < 0 || collect > 2) throw std::runtime_error("set_collection: invalid mode");
         const bool changed = collect != h->collect || (collect_state != 0) != (h->collect_state != 0);
@@ -695,6 +594,7 @@ int shyft_hip_set_collection(shyft_hip_region* h, int collect, int collect_state
 
 int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, size_t n) {
     if (!h) return fail(h, "shyft_hip_set_catchment_filter: null handle");
+    if (h->sh) return guarded(h, [&] { shards::set_catchment_filter(h->sh, cids, n); });
     return guarded(h, [&] {
         if (n == 0) {
             h->active.clear();
@@ -718,6 +618,7 @@ int shyft_hip_set_catchment_filter(shyft_hip_region* h, const int64_t* cids, siz
 
 int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_fields) {
     if (!h || !state) return fail(h, "shyft_hip_set_state: null argument");
+    if (h->sh) return guarded(h, [&] { shards::set_state(h->sh, state, n_fields); });
     return guarded(h, [&] {
         if (n_fields != h->n_state_fields()) throw std::runtime_error("set_state: wrong number of state fields");
         const size_t N = h->n;
@@ -731,6 +632,11 @@ int shyft_hip_set_state(shyft_hip_region* h, const double* state, size_t n_field
 
 int shyft_hip_copy_state(shyft_hip_region* dst, const shyft_hip_region* src) {
     if (!dst || !src) return fail(dst, "shyft_hip_copy_state: null argument");
+    if (dst->sh || src->sh)
+        return guarded(dst, [&] {
+            if (!dst->sh || !src->sh) throw std::runtime_error("copy_state: one region is sharded, the other is not");
+            shards::copy_state(dst->sh, src->sh);
+        });
     return guarded(dst, [&] {
         if (src->stack != dst->stack || src->n != dst->n)
             throw std::runtime_error("copy_state: regions differ in method stack or number of cells");
@@ -758,6 +664,7 @@ int shyft_hip_copy_state(shyft_hip_region* dst, const shyft_hip_region* src) {
 int shyft_hip_get_state(const shyft_hip_region* hc, double* state, size_t n_fields) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !state) return fail(h, "shyft_hip_get_state: null argument");
+    if (h->sh) return guarded(h, [&] { shards::get_state(h->sh, state, n_fields); });
     return guarded(h, [&] {
         if (n_fields != h->n_state_fields()) throw std::runtime_error("get_state: wrong number of state fields");
         const size_t N = h->n;
@@ -770,6 +677,7 @@ int shyft_hip_get_state(const shyft_hip_region* hc, double* state, size_t n_fiel
 
 int shyft_hip_set_forcing(shyft_hip_region* h, int var, size_t step0, size_t n, const double* src, int src_on_device) {
     if (!h || !src) return fail(h, "shyft_hip_set_forcing: null argument");
+    if (h->sh) return guarded(h, [&] { shards::set_forcing(h->sh, var, step0, n, src, src_on_device); });
     return guarded(h, [&] {
         if (var < 0 || var >= N_FORCING) throw std::runtime_error("set_forcing: invalid variable");
         check_window(h, step0, n, "set_forcing");
@@ -781,6 +689,7 @@ int shyft_hip_set_forcing(shyft_hip_region* h, int var, size_t step0, size_t n, 
 int shyft_hip_get_forcing(const shyft_hip_region* hc, int var, size_t step0, size_t n, double* dst, int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_get_forcing: null argument");
+    if (h->sh) return guarded(h, [&] { shards::get_rows(h->sh, 0, var, step0, n, dst, dst_on_device); });
     return guarded(h, [&] {
         if (var < 0 || var >= N_FORCING) throw std::runtime_error("get_forcing: invalid variable");
         check_window(h, step0, n, "get_forcing");
@@ -791,6 +700,7 @@ int shyft_hip_get_forcing(const shyft_hip_region* hc, int var, size_t step0, siz
 
 int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n) {
     if (!h) return fail(h, "shyft_hip_synthetic_forcing: null handle");
+    if (h->sh) return guarded(h, [&] { shards::synthetic_forcing(h->sh, seed, cell_offset, step0, n); });
     return guarded(h, [&] {
         check_window(h, step0, n, "synthetic_forcing");
         if (!h->has_geo) throw std::runtime_error("synthetic_forcing: geo_cell_data not set");
@@ -805,6 +715,7 @@ int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cel
 int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cell_offset, size_t w0_next,
                                          int n_cus) {
     if (!h) return fail(h, "shyft_hip_prefetch_synthetic_forcing: null handle");
+    if (h->sh) return guarded(h, [&] { shards::prefetch_synthetic_forcing(h->sh, seed, cell_offset, w0_next, n_cus); });
     return guarded(h, [&] {
         if (h->T == 0 || h->TW == 0) throw std::runtime_error("prefetch_synthetic_forcing: no time axis");
         if (w0_next + h->TW > h->T) throw std::runtime_error("prefetch_synthetic_forcing: window beyond the time axis");
@@ -848,6 +759,7 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
 
 int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next) {
     if (!h) return fail(h, "shyft_hip_swap_forcing_window: null handle");
+    if (h->sh) return guarded(h, [&] { shards::swap_forcing_window(h->sh, w0_next); });
     return guarded(h, [&] {
         if (h->gen_w0 != w0_next) throw std::runtime_error("swap_forcing_window: no prefetched window at this step");
         if (h->d_forcing_next.n != h->d_forcing.n || w0_next + h->TW > h->T)
@@ -867,6 +779,7 @@ int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next) {
 int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const double* src_xyz, const double* src_values,
                           size_t step0, size_t n, const double* idw_param) {
     if (!h || !src_xyz || !src_values || !idw_param) return fail(h, "shyft_hip_interpolate: null argument");
+    if (h->sh) return guarded(h, [&] { shards::interpolate(h->sh, var, n_sources, src_xyz, src_values, step0, n, idw_param); });
     return guarded(h, [&] {
         if (var < 0 || var >= N_FORCING) throw std::runtime_error("interpolate: invalid variable");
         if (!h->has_geo) throw std::runtime_error("interpolate: geo_cell_data not set");
@@ -986,6 +899,7 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
 
 int shyft_hip_interpolation_path(const shyft_hip_region* h, int var) {
     if (!h || var < 0 || var >= N_FORCING) return -1;
+    if (h->sh) return shards::interpolation_path(h->sh, var);
     return h->idw[var].last_path;
 }
 
@@ -999,6 +913,7 @@ void check_btk_param(const double* p) {
 int shyft_hip_interpolate_btk(shyft_hip_region* h, size_t n_sources, const double* src_xyz, const double* src_values,
                               size_t step0, size_t n, const double* prior_gradient, const double* btk_param) {
     if (!h || !src_xyz || !src_values || !btk_param) return fail(h, "shyft_hip_interpolate_btk: null argument");
+    if (h->sh) return guarded(h, [&] { shards::interpolate_btk(h->sh, n_sources, src_xyz, src_values, step0, n, prior_gradient, btk_param); });
     return guarded(h, [&] {
         if (!h->has_geo) throw std::runtime_error("interpolate: geo_cell_data not set");
         if (n_sources == 0) throw std::runtime_error("interpolate: no sources");
@@ -1226,15 +1141,9 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
     a.active = h->active.empty() ? nullptr : h->d_active.p;
     a.err = h->d_err.p;
-    a.hand = nullptr;
-    if (SHYFT_PTGSK_SPLIT) {
-        h->d_hand.alloc(2 * h->TW * h->n);
-        a.hand = h->d_hand.p;
-    }
     hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
-    hip_check(launch_ptgsk_run(a, h->stream, SHYFT_PTGSK_SPLIT ? h->ev_mid : nullptr), "ptgsk_run_kernel launch");
+    hip_check(launch_ptgsk_run(a, h->stream), "ptgsk_run_kernel launch");
     hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
-    h->last_parts = SHYFT_PTGSK_SPLIT ? 2 : 1;
 }
 
 static void finish_run(shyft_hip_region* h) {
@@ -1245,14 +1154,6 @@ static void finish_run(shyft_hip_region* h) {
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
     h->last_ms = ms;
-    h->last_part_ms[0] = ms;
-    h->last_part_ms[1] = 0.0;
-    if (h->last_parts == 2) {
-        float m0 = 0.f;
-        hip_check(hipEventElapsedTime(&m0, h->ev0, h->ev_mid), "hipEventElapsedTime");
-        h->last_part_ms[0] = m0;
-        h->last_part_ms[1] = ms - m0;
-    }
     // the per-cell error codes stay on the device: one reduction to the lowest failing cell, 8 bytes back
     const int32_t none = INT32_MAX;
     hip_check(hipMemcpyAsync(h->d_flag.p, &none, sizeof(int32_t), hipMemcpyHostToDevice, h->stream), "upload flag");
@@ -1300,6 +1201,7 @@ static void check_run_args(const shyft_hip_region* h, size_t use_ncore, int star
 
 int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, int n_steps) {
     if (!h) return fail(h, "shyft_hip_run_cells: null handle");
+    if (h->sh) return guarded(h, [&] { shards::run_cells(h->sh, use_ncore, start_step, n_steps); });
     return guarded(h, [&] {
         check_run_args(h, use_ncore, start_step, n_steps);
         launch_run(h, start_step, n_steps);
@@ -1309,6 +1211,7 @@ int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, i
 
 int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps) {
     if (!h) return fail(h, "shyft_hip_run_cells_async: null handle");
+    if (h->sh) return guarded(h, [&] { shards::run_cells_async(h->sh, start_step, n_steps); });
     return guarded(h, [&] {
         check_run_args(h, 0, start_step, n_steps);
         launch_run(h, start_step, n_steps);
@@ -1317,20 +1220,23 @@ int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps) 
 
 int shyft_hip_synchronize(shyft_hip_region* h) {
     if (!h) return fail(h, "shyft_hip_synchronize: null handle");
+    if (h->sh) return guarded(h, [&] { shards::synchronize(h->sh); });
     return guarded(h, [&] { finish_run(h); });
 }
 
-double shyft_hip_last_run_ms(const shyft_hip_region* h) { return h ? h->last_ms : 0.0; }
+double shyft_hip_last_run_ms(const shyft_hip_region* h) { return h ? (h->sh ? shards::last_run_ms(h->sh) : h->last_ms) : 0.0; }
 
 int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n) {
     if (!h) return 0;
-    for (int k = 0; k < n && k < h->last_parts; ++k) ms[k] = h->last_part_ms[k];
-    return h->last_parts;
+    if (h->sh) return shards::last_run_kernel_ms(h->sh, ms, n);
+    if (n > 0) ms[0] = h->last_ms;  // every stack runs one kernel per run_cells
+    return 1;
 }
 
 int shyft_hip_get_series(const shyft_hip_region* hc, int series, size_t step0, size_t n, double* dst, int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_get_series: null argument");
+    if (h->sh) return guarded(h, [&] { shards::get_rows(h->sh, 1, series, step0, n, dst, dst_on_device); });
     return guarded(h, [&] {
         if (series < 0 || size_t(series) >= h->n_series())
             throw std::runtime_error("get_series: series not collected in this collection mode");
@@ -1344,6 +1250,7 @@ int shyft_hip_get_state_series(const shyft_hip_region* hc, int field, size_t ste
                                int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_get_state_series: null argument");
+    if (h->sh) return guarded(h, [&] { shards::get_rows(h->sh, 2, field, step0, n, dst, dst_on_device); });
     return guarded(h, [&] {
         if (!h->collect_state) throw std::runtime_error("get_state_series: state collection is off");
         if (field < 0 || size_t(field) >= h->n_state_series()) throw std::runtime_error("get_state_series: invalid field");
@@ -1353,20 +1260,22 @@ int shyft_hip_get_state_series(const shyft_hip_region* hc, int field, size_t ste
     });
 }
 
-int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* ids, size_t n_ids, int scope, int weighted,
-                         size_t step0, size_t n, double* dst) {
-    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
-    if (!h || !dst) return fail(h, "shyft_hip_statistics: null argument");
+}  // extern "C"
+namespace shyft_hip_impl {
+int region_selected_sums(shyft_hip_region* h, int series, const int64_t* ids, size_t n_ids, int scope, int weighted,
+                         size_t step0, size_t n, double* dst, double* sum_area_out, size_t* n_selected) {
     return guarded(h, [&] {
         const double* src = series_rows(h, series, step0, n, "statistics");
         std::vector<int32_t> sel = select_cells(h, ids, n_ids, scope);
-        if (sel.empty()) {  // no match: sum -> empty ts in the reference; average -> nan
-            for (size_t t = 0; t < n; ++t) dst[t] = weighted ? NAN : 0.0;
+        if (n_selected) *n_selected = sel.size();
+        double sum_area = 0.0;
+        if (sel.empty()) {
+            for (size_t t = 0; t < n; ++t) dst[t] = 0.0;
+            if (sum_area_out) *sum_area_out = 0.0;
             return;
         }
         h->d_sel.alloc(std::max(h->d_sel.n, sel.size()));
         hip_check(region_copy(h, h->d_sel.p, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload sel");
-        double sum_area = 0.0;
         const double* w = nullptr;
         if (weighted) {
             std::vector<double> a(sel.size());
@@ -1381,17 +1290,35 @@ int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* 
         h->d_tmp.alloc(std::max(h->d_tmp.n, n));
         hip_check(launch_select_sum(src, h->n, n, h->d_sel.p, sel.size(), w, h->d_tmp.p, h->stream), "select_sum");
         copy_rows(h->stream, dst, h->d_tmp.p, n * sizeof(double), 0, 1);
-        if (weighted) {
-            const double s = 1 / sum_area;  // scale_by(1/sum_area) (cell_model.h:252)
-            for (size_t t = 0; t < n; ++t) dst[t] *= s;
-        }
+        if (sum_area_out) *sum_area_out = sum_area;
     });
+}
+}  // namespace shyft_hip_impl
+extern "C" {
+
+int shyft_hip_statistics(const shyft_hip_region* hc, int series, const int64_t* ids, size_t n_ids, int scope, int weighted,
+                         size_t step0, size_t n, double* dst) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || !dst) return fail(h, "shyft_hip_statistics: null argument");
+    if (h->sh) return guarded(h, [&] { shards::statistics(h->sh, series, ids, n_ids, scope, weighted, step0, n, dst); });
+    double sum_area = 0.0;
+    size_t n_sel = 0;
+    const int rc = region_selected_sums(h, series, ids, n_ids, scope, weighted, step0, n, dst, &sum_area, &n_sel);
+    if (rc || !weighted) return rc;
+    if (n_sel == 0) {  // no match: sum -> empty ts in the reference (0 here); average -> nan
+        for (size_t t = 0; t < n; ++t) dst[t] = NAN;
+        return 0;
+    }
+    const double s = 1 / sum_area;  // scale_by(1/sum_area) (cell_model.h:252)
+    for (size_t t = 0; t < n; ++t) dst[t] *= s;
+    return 0;
 }
 
 int shyft_hip_catchment_sums(const shyft_hip_region* hc, int series, size_t step0, size_t n, double* dst,
                              int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_catchment_sums: null argument");
+    if (h->sh) return guarded(h, [&] { shards::catchment_sums(h->sh, series, step0, n, dst, dst_on_device, false); });
     return guarded(h, [&] {
         const double* src = series_rows(h, series, step0, n, "catchment_sums");
         const size_t C = h->cix_to_cid.size();
@@ -1410,6 +1337,7 @@ int shyft_hip_catchment_area_sums(const shyft_hip_region* hc, int series, size_t
                                   int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_catchment_area_sums: null argument");
+    if (h->sh) return guarded(h, [&] { shards::catchment_sums(h->sh, series, step0, n, dst, dst_on_device, true); });
     return guarded(h, [&] {
         const double* src = series_rows(h, series, step0, n, "catchment_area_sums");
         update_derived(h);  // per-cell constants (cell area) are current
@@ -1427,10 +1355,16 @@ int shyft_hip_catchment_area_sums(const shyft_hip_region* hc, int series, size_t
     });
 }
 
-size_t shyft_hip_number_of_catchments(const shyft_hip_region* h) { return h ? h->cix_to_cid.size() : 0; }
+size_t shyft_hip_number_of_catchments(const shyft_hip_region* h) {
+    return h ? (h->sh ? shards::number_of_catchments(h->sh) : h->cix_to_cid.size()) : 0;
+}
 
 int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids) {
     if (!h || !cids) return fail(const_cast<shyft_hip_region*>(h), "shyft_hip_catchment_ids: null argument");
+    if (h->sh) {
+        shards::catchment_ids(h->sh, cids);
+        return 0;
+    }
     for (size_t c = 0; c < h->cix_to_cid.size(); ++c) cids[c] = h->cix_to_cid[c];
     return 0;
 }
@@ -1438,6 +1372,19 @@ int shyft_hip_catchment_ids(const shyft_hip_region* h, int64_t* cids) {
 int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out) {
     if (!src || !out) return fail(nullptr, "shyft_hip_region_clone: null argument");
     *out = nullptr;
+    if (src->sh) {
+        try {
+            std::unique_ptr<shyft_hip_region> c(new shyft_hip_region());
+            c->stack = src->stack;
+            c->n = src->n;
+            c->device = src->device;
+            c->sh = shards::clone(src->sh);
+            *out = c.release();
+            return 0;
+        } catch (const std::exception& e) {
+            return fail(nullptr, e.what());
+        }
+    }
     shyft_hip_region* c = nullptr;
     if (shyft_hip_region_create(src->stack, src->n, src->device, &c)) return 1;
     std::unique_ptr<shyft_hip_region, void (*)(shyft_hip_region*)> h(c, shyft_hip_region_destroy);
@@ -1473,6 +1420,7 @@ int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out) 
 
 int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t step0, size_t n, double* buf, int write) {
     if (!h || !buf) return fail(h, "shyft_hip_cell_series: null argument");
+    if (h->sh) return guarded(h, [&] { shards::cell_series(h->sh, series, cell, step0, n, buf, write); });
     return guarded(h, [&] {
         if (cell >= h->n) throw std::runtime_error("cell_series: cell index out of range");
         if (write && series < SHYFT_HIP_SERIES_FORCING)
@@ -1493,6 +1441,7 @@ int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t s
 int shyft_hip_forcing_ok(const shyft_hip_region* hc, int* ok) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !ok) return fail(h, "shyft_hip_forcing_ok: null argument");
+    if (h->sh) return guarded(h, [&] { shards::forcing_ok(h->sh, ok); });
     return guarded(h, [&] {
         *ok = 0;
         if (h->T == 0) throw std::runtime_error("is_cell_env_ts_ok: no time axis (initialize_cell_environment)");
@@ -1513,6 +1462,7 @@ extern "C" {
 
 int shyft_hip_set_routing_groups(shyft_hip_region* h, const int32_t* group_of_cell, size_t n_groups) {
     if (!h) return fail(h, "shyft_hip_set_routing_groups: null handle");
+    if (h->sh) return guarded(h, [&] { shards::set_routing_groups(h->sh, group_of_cell, n_groups); });
     return guarded(h, [&] {
         if (n_groups > 0 && !group_of_cell) throw std::runtime_error("set_routing_groups: group_of_cell is null");
         std::vector<int32_t> off(n_groups + 1, 0), cells;
@@ -1539,6 +1489,7 @@ int shyft_hip_set_routing_groups(shyft_hip_region* h, const int32_t* group_of_ce
 int shyft_hip_routing_group_sums(const shyft_hip_region* hc, size_t step0, size_t n, double* dst, int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_routing_group_sums: null argument");
+    if (h->sh) return guarded(h, [&] { shards::routing_group_sums(h->sh, step0, n, dst, dst_on_device); });
     return guarded(h, [&] {
         const size_t G = h->n_route_groups;
         if (G == 0) return;
@@ -1677,6 +1628,7 @@ extern "C" {
 int shyft_hip_ensemble_run(shyft_hip_region* h, const double* params, size_t n_members, size_t n_per_set,
                            int start_step, int n_steps, int collect) {
     if (!h || !params) return fail(h, "shyft_hip_ensemble_run: null argument");
+    if (h->sh) return guarded(h, [&] { shards::ensemble_run(h->sh, params, n_members, n_per_set, start_step, n_steps, collect); });
     return guarded(h, [&] {
         if (n_members == 0) throw std::runtime_error("ensemble_run: n_members must be > 0");
         if (collect != COLLECT_DISCHARGE && collect != COLLECT_DISCHARGE_SNOW)
@@ -1763,6 +1715,7 @@ int shyft_hip_ensemble_sums(const shyft_hip_region* hc, int series, int area_wei
                             double* dst, int dst_on_device) {
     shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
     if (!h || !dst) return fail(h, "shyft_hip_ensemble_sums: null argument");
+    if (h->sh) return guarded(h, [&] { shards::ensemble_sums(h->sh, series, area_weighted, step0, n, dst, dst_on_device); });
     return guarded(h, [&] {
         shyft_hip_region* x = h->ens;
         if (!x || h->ens_members == 0) throw std::runtime_error("ensemble_sums: no ensemble run");
@@ -1786,6 +1739,9 @@ int shyft_hip_ensemble_sums(const shyft_hip_region* hc, int series, int area_wei
     });
 }
 
-double shyft_hip_ensemble_last_ms(const shyft_hip_region* h) { return h && h->ens ? h->ens->last_ms : 0.0; }
+double shyft_hip_ensemble_last_ms(const shyft_hip_region* h) {
+    if (h && h->sh) return shards::ensemble_last_ms(h->sh);
+    return h && h->ens ? h->ens->last_ms : 0.0;
+}
 
 }  // extern "C"

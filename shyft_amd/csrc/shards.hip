@@ -1,0 +1,596 @@
+// Sharded regions: one region_model whose cells are split into contiguous shards, each shard an ordinary region
+// (region.hip) on its own device (or several shards on one device), driven from one host process.
+//
+// The reference runs a whole region in one process and sums every catchment over all of its cells
+// (core/region_model.h:972-1021 parallel_run, core/cell_model.h:308-333 cell_statistics, core/routing.h:344-383
+// river inflows). Here run_cells is per-cell independent, so each shard runs its cells on its device with no
+// data-path exchange; the only cross-shard step is the combination of per-catchment / per-routing-group partial
+// sums:
+//   - every shard reduces its cells into [rows][steps] partials on its device (the deterministic segment sums of
+//     region.hip), scattered to the region's global row order;
+//   - the partials are all-gathered: RCCL ncclAllGather over xGMI when every shard has its own device (one
+//     communicator per device from ncclCommInitAll), device-to-device copies when shards share a device;
+//   - each device adds the gathered partials in shard order (fixed order: deterministic, and bit-equal to the
+//     unsharded region wherever a catchment / group lies inside one shard, since the other partials are +0.0).
+// Host-side fan-out runs the shards' calls on one host thread per shard, so the devices work concurrently.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <exception>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "include_internal/region_impl.h"
+#include "include_internal/shards.h"
+
+namespace shyft_hip_impl {
+
+struct shard_bufs {
+    dbuf<double> part, full, gath, out;  // child partial [R_k][n], scattered [R][n], gathered [S][R][n], sum [R][n]
+    dbuf<int32_t> rows;                  // child row -> global row
+};
+
+struct shard_set {
+    int stack = 0;
+    size_t n = 0;
+    std::vector<shyft_hip_region*> r;  // owned
+    std::vector<size_t> b, e;          // cell range of each shard
+    std::vector<int> dev;
+    std::vector<char> idle;            // no calculated cell under the catchment filter: not run, not interpolated
+    std::vector<int64_t> cix_to_cid;   // the region's catchments in first-appearance order (region_model.h:236-252)
+    std::map<int64_t, size_t> cid_to_cix;
+    std::vector<std::vector<int64_t>> child_cids;
+    size_t n_groups = 0;               // routing groups
+    std::vector<ncclComm_t> comms;     // one per shard when the devices are distinct
+    std::vector<hipStream_t> streams;  // one per shard, on its device
+    std::vector<std::unique_ptr<shard_bufs>> bufs;
+    int path = SHYFT_HIP_COMBINE_COPY;
+    size_t ens_members = 0;
+
+    size_t S() const { return r.size(); }
+    size_t shard_of(size_t cell) const {
+        return size_t(std::upper_bound(b.begin(), b.end(), cell) - b.begin()) - 1;
+    }
+};
+
+namespace {
+
+void ck(shyft_hip_region* child, int rc) {
+    if (rc) throw std::runtime_error(shyft_hip_last_error(child));
+}
+
+void nccl_check(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// f(k) for every shard, shard k on its own host thread with its device current; the first error is rethrown
+template <class F>
+void for_shards(shard_set* s, F&& f, bool parallel = true) {
+    const size_t S = s->S();
+    std::vector<std::string> errs(S);
+    auto one = [&](size_t k) {
+        try {
+            hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+            f(k);
+        } catch (const std::exception& e) {
+            errs[k] = e.what();
+        }
+    };
+    if (!parallel || S == 1) {
+        for (size_t k = 0; k < S; ++k) one(k);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 1; k < S; ++k) th.emplace_back(one, k);
+        one(0);
+        for (auto& t : th) t.join();
+    }
+    for (size_t k = 0; k < S; ++k)
+        if (!errs[k].empty()) throw std::runtime_error(errs[k]);
+}
+
+// rows of a [n][N] host array <-> the [n][n_k] block of shard k
+void split_cols(const double* src, size_t N, size_t n, size_t b, size_t nk, std::vector<double>& dst) {
+    dst.resize(n * nk);
+    for (size_t t = 0; t < n; ++t) std::copy(src + t * N + b, src + t * N + b + nk, dst.begin() + t * nk);
+}
+void join_cols(const std::vector<double>& src, size_t N, size_t n, size_t b, size_t nk, double* dst) {
+    for (size_t t = 0; t < n; ++t) std::copy(src.begin() + t * nk, src.begin() + (t + 1) * nk, dst + t * N + b);
+}
+
+// The combination of per-shard partial sums (see the file header). part(k, dev_ptr) writes shard k's partial
+// [R_k][n] to a device buffer on its device and returns R_k; rowmap(k) maps its rows to the R global rows (empty:
+// identity, R_k == R). The result [R][n] is written to dst (host, or a device pointer on shard 0's device).
+// skip_idle: an idle shard (no calculated cell) contributes zeros instead of calling part (ensembles: it ran none);
+// otherwise its cells count like any others (catchment sums over uncalculated cells, as the unsharded region)
+template <class Part, class RowMap>
+void combine(shard_set* s, size_t R, size_t n, Part&& part, RowMap&& rowmap, double* dst, int dst_on_device,
+             bool skip_idle = false) {
+    const size_t S = s->S(), M = R * n;
+    if (M == 0) return;
+    for_shards(s, [&](size_t k) {
+        shard_bufs& q = *s->bufs[k];
+        const std::vector<int32_t> map = rowmap(k);
+        const size_t Rk = map.empty() ? R : map.size();
+        q.full.alloc(M);
+        q.gath.alloc(S * M);
+        q.out.alloc(M);
+        if ((skip_idle && s->idle[k]) || Rk == 0) {
+            hip_check(hipMemsetAsync(q.full.p, 0, M * sizeof(double), s->streams[k]), "memset");
+        } else if (map.empty()) {
+            part(k, q.full.p);  // synchronous on the shard's stream
+        } else {
+            q.part.alloc(Rk * n);
+            q.rows.alloc(Rk);
+            part(k, q.part.p);
+            hip_check(hipMemcpyAsync(q.rows.p, map.data(), Rk * sizeof(int32_t), hipMemcpyHostToDevice, s->streams[k]),
+                      "upload rows");
+            hip_check(hipMemsetAsync(q.full.p, 0, M * sizeof(double), s->streams[k]), "memset");
+            hip_check(launch_scatter_rows(q.part.p, q.rows.p, Rk, n, q.full.p, s->streams[k]), "scatter_rows");
+        }
+        hip_check(hipStreamSynchronize(s->streams[k]), "partials");
+    });
+    if (s->path == SHYFT_HIP_COMBINE_RCCL) {
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        for (size_t k = 0; k < S; ++k) {
+            hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+            nccl_check(ncclAllGather(s->bufs[k]->full.p, s->bufs[k]->gath.p, M, ncclDouble, s->comms[k], s->streams[k]),
+                       "ncclAllGather");
+        }
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        // every device holds the same gathered partials; shard 0's device sums them for the caller
+        hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
+    } else {
+        hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
+        for (size_t k = 0; k < S; ++k)
+            hip_check(hipMemcpyPeerAsync(s->bufs[0]->gath.p + k * M, s->dev[0], s->bufs[k]->full.p, s->dev[k],
+                                         M * sizeof(double), s->streams[0]),
+                      "gather partials");
+    }
+    shard_bufs& q0 = *s->bufs[0];
+    double* out = dst_on_device ? dst : q0.out.p;
+    hip_check(launch_ordered_sum(q0.gath.p, S, M, out, s->streams[0]), "ordered_sum");
+    if (!dst_on_device)
+        hip_check(hipMemcpyAsync(dst, q0.out.p, M * sizeof(double), hipMemcpyDeviceToHost, s->streams[0]), "download");
+    for (size_t k = 0; k < S; ++k) {  // RCCL: every stream; copies: stream 0
+        hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+        hip_check(hipStreamSynchronize(s->streams[k]), "combine");
+    }
+}
+
+// the region's catchment map from its geo rows (cid = int(geo[4]), first appearance in cell order)
+void map_catchments(shard_set* s, const double* geo11) {
+    s->cix_to_cid.clear();
+    s->cid_to_cix.clear();
+    for (size_t i = 0; i < s->n; ++i) {
+        const int64_t c = int64_t(int(geo11[i * 11 + 4]));
+        if (s->cid_to_cix.emplace(c, s->cix_to_cid.size()).second) s->cix_to_cid.push_back(c);
+    }
+    s->child_cids.assign(s->S(), {});
+    for (size_t k = 0; k < s->S(); ++k) {
+        s->child_cids[k].resize(shyft_hip_number_of_catchments(s->r[k]));
+        ck(s->r[k], shyft_hip_catchment_ids(s->r[k], s->child_cids[k].data()));
+    }
+}
+
+std::vector<int32_t> catchment_rows(const shard_set* s, size_t k) {
+    std::vector<int32_t> m;
+    for (int64_t c : s->child_cids[k]) m.push_back(int32_t(s->cid_to_cix.at(c)));
+    return m;
+}
+
+}  // namespace
+
+shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_t n_shards) {
+    if (n_shards == 0 || !devices) throw std::runtime_error("shyft_hip_region_create_sharded: no devices");
+    if (n_cells < n_shards) throw std::runtime_error("shyft_hip_region_create_sharded: fewer cells than shards");
+    int n_dev = 0;
+    hip_check(hipGetDeviceCount(&n_dev), "hipGetDeviceCount");
+    for (size_t k = 0; k < n_shards; ++k)
+        if (devices[k] < 0 || devices[k] >= n_dev)
+            throw std::runtime_error("shyft_hip_region_create_sharded: device " + std::to_string(devices[k]) +
+                                     " does not exist (" + std::to_string(n_dev) + " visible)");
+    std::unique_ptr<shard_set, void (*)(shard_set*)> s(new shard_set(), shard_set_destroy);
+    s->stack = stack;
+    s->n = n_cells;
+    for (size_t k = 0; k < n_shards; ++k) {
+        const size_t b = n_cells * k / n_shards, e = n_cells * (k + 1) / n_shards;
+        shyft_hip_region* c = nullptr;
+        if (shyft_hip_region_create(stack, e - b, devices[k], &c)) throw std::runtime_error(shyft_hip_last_error(nullptr));
+        s->r.push_back(c);
+        s->b.push_back(b);
+        s->e.push_back(e);
+        s->dev.push_back(devices[k]);
+        s->idle.push_back(0);
+        hipStream_t st = nullptr;
+        hip_check(hipSetDevice(devices[k]), "hipSetDevice");
+        hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        s->streams.push_back(st);
+        s->bufs.emplace_back(new shard_bufs());
+    }
+    std::vector<int> sorted(s->dev);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (n_shards > 1 && distinct) {
+        s->comms.resize(n_shards);
+        nccl_check(ncclCommInitAll(s->comms.data(), int(n_shards), s->dev.data()), "ncclCommInitAll");
+        s->path = SHYFT_HIP_COMBINE_RCCL;
+    } else {
+        // shards sharing a device (or one shard): the partials are copied device to device (hipMemcpyPeerAsync),
+        // RCCL does not put two ranks of one communicator on one device
+        s->path = SHYFT_HIP_COMBINE_COPY;
+    }
+    return s.release();
+}
+
+void shard_set_destroy(shard_set* s) {
+    if (!s) return;
+    for (auto& c : s->comms) (void)ncclCommDestroy(c);
+    for (size_t k = 0; k < s->streams.size(); ++k) {
+        (void)hipSetDevice(s->dev[k]);
+        (void)hipStreamSynchronize(s->streams[k]);
+        s->bufs[k].reset();  // device buffers freed on their device
+        (void)hipStreamDestroy(s->streams[k]);
+    }
+    for (auto* c : s->r) shyft_hip_region_destroy(c);
+    delete s;
+}
+
+namespace shards {
+
+size_t info(const shard_set* s, size_t k, int* device, size_t* cell0, size_t* n_cells) {
+    if (k < s->S()) {
+        if (device) *device = s->dev[k];
+        if (cell0) *cell0 = s->b[k];
+        if (n_cells) *n_cells = s->e[k] - s->b[k];
+    }
+    return s->S();
+}
+
+int combine_path(const shard_set* s) { return s->path; }
+
+void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double* rdist) {
+    for_shards(s, [&](size_t k) {
+        ck(s->r[k], shyft_hip_set_geo(s->r[k], geo11 + s->b[k] * 11, rid ? rid + s->b[k] : nullptr,
+                                      rdist ? rdist + s->b[k] : nullptr));
+    });
+    map_catchments(s, geo11);
+    std::fill(s->idle.begin(), s->idle.end(), 0);  // set_geo clears the filter state of each shard
+}
+
+void set_parameters(shard_set* s, const double* params, size_t n_sets, size_t n_per_set, const int32_t* set_ix) {
+    for_shards(s, [&](size_t k) {
+        ck(s->r[k], shyft_hip_set_parameters(s->r[k], params, n_sets, n_per_set, set_ix ? set_ix + s->b[k] : nullptr));
+    });
+}
+
+void set_time_axis(shard_set* s, int64_t t0, int64_t dt, size_t n_steps, size_t window) {
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_set_time_axis(s->r[k], t0, dt, n_steps, window)); });
+}
+
+void move_window(shard_set* s, size_t w0, int fill_mask) {
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_move_window(s->r[k], w0, fill_mask)); });
+}
+
+void set_collection(shard_set* s, int collect, int collect_state) {
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_set_collection(s->r[k], collect, collect_state)); });
+}
+
+// region_model::set_catchment_calculation_filter (region_model.h:356-370) over the whole region: checked against
+// the region's catchments, then each shard gets the filtered catchments it holds; a shard holding none is idle
+void set_catchment_filter(shard_set* s, const int64_t* cids, size_t n) {
+    if (n > 0) {
+        if (n > s->cix_to_cid.size())
+            throw std::runtime_error("set_catchment_calculation_filter: supplied list > available catchments");
+        for (size_t j = 0; j < n; ++j)
+            if (s->cid_to_cix.find(cids[j]) == s->cid_to_cix.end())
+                throw std::runtime_error("set_catchment_calculation_filter: no cells have supplied cid");
+    }
+    for_shards(s, [&](size_t k) {
+        std::vector<int64_t> mine;
+        for (size_t j = 0; j < n; ++j)
+            if (std::find(s->child_cids[k].begin(), s->child_cids[k].end(), cids[j]) != s->child_cids[k].end())
+                mine.push_back(cids[j]);
+        s->idle[k] = n > 0 && mine.empty();
+        ck(s->r[k], shyft_hip_set_catchment_filter(s->r[k], mine.empty() ? nullptr : mine.data(), mine.size()));
+    });
+}
+
+void set_state(shard_set* s, const double* state, size_t n_fields) {
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_set_state(s->r[k], state + s->b[k] * n_fields, n_fields)); });
+}
+
+void get_state(shard_set* s, double* state, size_t n_fields) {
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_get_state(s->r[k], state + s->b[k] * n_fields, n_fields)); });
+}
+
+void copy_state(shard_set* d, const shard_set* src) {
+    if (d->S() != src->S() || d->b != src->b) throw std::runtime_error("copy_state: regions are sharded differently");
+    for_shards(d, [&](size_t k) { ck(d->r[k], shyft_hip_copy_state(d->r[k], src->r[k])); });
+}
+
+void set_forcing(shard_set* s, int var, size_t step0, size_t n, const double* src, int on_device) {
+    if (on_device) throw std::runtime_error("set_forcing: a sharded region takes forcing from host memory");
+    for_shards(s, [&](size_t k) {
+        std::vector<double> blk;
+        split_cols(src, s->n, n, s->b[k], s->e[k] - s->b[k], blk);
+        ck(s->r[k], shyft_hip_set_forcing(s->r[k], var, step0, n, blk.data(), 0));
+    });
+}
+
+// get_forcing (what 0), get_series (1), get_state_series (2) into host [n][cells]
+void get_rows(shard_set* s, int what, int id, size_t step0, size_t n, double* dst, int on_device) {
+    if (on_device) throw std::runtime_error("a sharded region returns series to host memory");
+    for_shards(s, [&](size_t k) {
+        const size_t nk = s->e[k] - s->b[k];
+        std::vector<double> blk(n * nk);
+        shyft_hip_region* c = s->r[k];
+        ck(c, what == 0   ? shyft_hip_get_forcing(c, id, step0, n, blk.data(), 0)
+              : what == 1 ? shyft_hip_get_series(c, id, step0, n, blk.data(), 0)
+                          : shyft_hip_get_state_series(c, id, step0, n, blk.data(), 0));
+        join_cols(blk, s->n, n, s->b[k], nk, dst);
+    });
+}
+
+void interpolate(shard_set* s, int var, size_t n_sources, const double* xyz, const double* vals, size_t step0, size_t n,
+                 const double* prm) {
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k]) ck(s->r[k], shyft_hip_interpolate(s->r[k], var, n_sources, xyz, vals, step0, n, prm));
+    });
+}
+
+int interpolation_path(const shard_set* s, int var) {
+    // the gather of the shards that interpolated: none if one has not, tile if one ran tiles, copy if all copied
+    bool tile = false, copy = true, seen = false;
+    for (size_t k = 0; k < s->S(); ++k) {
+        if (s->idle[k]) continue;
+        const int q = shyft_hip_interpolation_path(s->r[k], var);
+        if (q <= SHYFT_HIP_IDW_NONE) return q;
+        seen = true;
+        tile = tile || q == SHYFT_HIP_IDW_TILE;
+        copy = copy && q == SHYFT_HIP_IDW_COPY;
+    }
+    if (!seen) return SHYFT_HIP_IDW_NONE;
+    return tile ? SHYFT_HIP_IDW_TILE : copy ? SHYFT_HIP_IDW_COPY : SHYFT_HIP_IDW_WAVE;
+}
+
+void interpolate_btk(shard_set* s, size_t n_sources, const double* xyz, const double* vals, size_t step0, size_t n,
+                     const double* prior, const double* prm) {
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k]) ck(s->r[k], shyft_hip_interpolate_btk(s->r[k], n_sources, xyz, vals, step0, n, prior, prm));
+    });
+}
+
+void synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n) {
+    for_shards(s, [&](size_t k) {
+        ck(s->r[k], shyft_hip_synthetic_forcing(s->r[k], seed, cell_offset + s->b[k], step0, n));
+    });
+}
+
+void prefetch_synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t w0_next, int n_cus) {
+    for_shards(s, [&](size_t k) {
+        ck(s->r[k], shyft_hip_prefetch_synthetic_forcing(s->r[k], seed, cell_offset + s->b[k], w0_next, n_cus));
+    });
+}
+
+void swap_forcing_window(shard_set* s, size_t w0_next) {
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_swap_forcing_window(s->r[k], w0_next)); });
+}
+
+// run_cells on every shard at once (region_model::parallel_run over the whole region, region_model.h:991-1021)
+void run_cells(shard_set* s, size_t use_ncore, int start_step, int n_steps) {
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k]) ck(s->r[k], shyft_hip_run_cells(s->r[k], use_ncore, start_step, n_steps));
+    });
+}
+
+void run_cells_async(shard_set* s, int start_step, int n_steps) {
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k]) ck(s->r[k], shyft_hip_run_cells_async(s->r[k], start_step, n_steps));
+    }, false);  // launches only: no threads needed
+}
+
+void synchronize(shard_set* s) {
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k]) ck(s->r[k], shyft_hip_synchronize(s->r[k]));
+    });
+}
+
+double last_run_ms(const shard_set* s) {
+    double m = 0.0;
+    for (size_t k = 0; k < s->S(); ++k)
+        if (!s->idle[k]) m = std::max(m, shyft_hip_last_run_ms(s->r[k]));
+    return m;
+}
+
+int last_run_kernel_ms(const shard_set* s, double* ms, int n) {
+    int parts = 1;
+    std::vector<double> mx(4, 0.0);
+    for (size_t k = 0; k < s->S(); ++k) {
+        double v[4] = {0, 0, 0, 0};
+        parts = shyft_hip_last_run_kernel_ms(s->r[k], v, 4);
+        for (int j = 0; j < 4; ++j) mx[size_t(j)] = std::max(mx[size_t(j)], v[j]);
+    }
+    for (int j = 0; j < n && j < parts; ++j) ms[j] = mx[size_t(j)];
+    return parts;
+}
+
+void cell_series(shard_set* s, int series, size_t cell, size_t step0, size_t n, double* buf, int write) {
+    if (cell >= s->n) throw std::runtime_error("cell_series: cell index out of range");
+    const size_t k = s->shard_of(cell);
+    hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+    ck(s->r[k], shyft_hip_cell_series(s->r[k], series, cell - s->b[k], step0, n, buf, write));
+}
+
+void forcing_ok(shard_set* s, int* ok) {
+    std::vector<int> oks(s->S(), 1);
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k]) ck(s->r[k], shyft_hip_forcing_ok(s->r[k], &oks[k]));
+    });
+    *ok = 1;
+    for (int v : oks) *ok = *ok && v;
+}
+
+// cell_statistics over the whole region (cell_model.h:228-333): the selection is resolved against the region
+// (cell indexes / catchment ids, verify_cids_exist), each shard sums its selected cells (value, or value x area
+// with the area sum for the weighted average), the partial sums are added in shard order
+void statistics(shard_set* s, int series, const int64_t* ids, size_t n_ids, int scope, int weighted, size_t step0,
+                size_t n, double* dst) {
+    std::vector<std::vector<int64_t>> sel(s->S());
+    std::vector<char> any(s->S(), n_ids == 0);
+    if (n_ids) {
+        for (size_t j = 0; j < n_ids; ++j) {
+            if (scope == SHYFT_HIP_SCOPE_CELL_IX) {
+                if (ids[j] < 0 || ids[j] > int64_t(s->n))
+                    throw std::runtime_error("Supplied cell index reference " + std::to_string(ids[j]) +
+                                             " is ouside valid range 0 .." + std::to_string(s->n));
+                if (ids[j] == int64_t(s->n)) continue;  // valid index, no cell (the reference's range check is <=)
+                const size_t k = s->shard_of(size_t(ids[j]));
+                sel[k].push_back(ids[j] - int64_t(s->b[k]));
+                any[k] = 1;
+            } else {
+                if (s->cid_to_cix.count(ids[j]) == 0)
+                    throw std::runtime_error("one or more supplied catchment_indexes does not exist:" +
+                                             std::to_string(ids[j]));
+                for (size_t k = 0; k < s->S(); ++k)
+                    if (std::find(s->child_cids[k].begin(), s->child_cids[k].end(), ids[j]) != s->child_cids[k].end()) {
+                        sel[k].push_back(ids[j]);
+                        any[k] = 1;
+                    }
+            }
+        }
+    }
+    std::vector<std::vector<double>> part(s->S(), std::vector<double>(n, 0.0));
+    std::vector<double> area(s->S(), 0.0);
+    for_shards(s, [&](size_t k) {
+        if (!any[k]) return;
+        ck(s->r[k], region_selected_sums(s->r[k], series, sel[k].empty() ? nullptr : sel[k].data(), sel[k].size(),
+                                         scope, weighted, step0, n, part[k].data(), &area[k], nullptr));
+    });
+    bool found = false;
+    double sum_area = 0.0;
+    for (size_t t = 0; t < n; ++t) dst[t] = 0.0;
+    for (size_t k = 0; k < s->S(); ++k) {
+        if (!any[k]) continue;
+        if (!found) {
+            for (size_t t = 0; t < n; ++t) dst[t] = part[k][t];
+            sum_area = area[k];
+            found = true;
+        } else {
+            for (size_t t = 0; t < n; ++t) dst[t] += part[k][t];
+            sum_area += area[k];
+        }
+    }
+    if (weighted) {
+        if (!found) {
+            for (size_t t = 0; t < n; ++t) dst[t] = NAN;
+            return;
+        }
+        const double f = 1 / sum_area;  // scale_by(1/sum_area) (cell_model.h:252)
+        for (size_t t = 0; t < n; ++t) dst[t] *= f;
+    }
+}
+
+void catchment_sums(shard_set* s, int series, size_t step0, size_t n, double* dst, int on_device, bool area) {
+    combine(
+        s, s->cix_to_cid.size(), n,
+        [&](size_t k, double* p) {
+            ck(s->r[k], area ? shyft_hip_catchment_area_sums(s->r[k], series, step0, n, p, 1)
+                             : shyft_hip_catchment_sums(s->r[k], series, step0, n, p, 1));
+        },
+        [&](size_t k) { return catchment_rows(s, k); }, dst, on_device);
+}
+
+size_t number_of_catchments(const shard_set* s) { return s->cix_to_cid.size(); }
+
+void catchment_ids(const shard_set* s, int64_t* cids) {
+    std::copy(s->cix_to_cid.begin(), s->cix_to_cid.end(), cids);
+}
+
+void set_routing_groups(shard_set* s, const int32_t* group_of_cell, size_t n_groups) {
+    for_shards(s, [&](size_t k) {
+        ck(s->r[k], shyft_hip_set_routing_groups(s->r[k], group_of_cell ? group_of_cell + s->b[k] : nullptr, n_groups));
+    });
+    s->n_groups = n_groups;
+}
+
+void routing_group_sums(shard_set* s, size_t step0, size_t n, double* dst, int on_device) {
+    combine(
+        s, s->n_groups, n,
+        [&](size_t k, double* p) { ck(s->r[k], shyft_hip_routing_group_sums(s->r[k], step0, n, p, 1)); },
+        [&](size_t) { return std::vector<int32_t>(); }, dst, on_device);
+}
+
+// parameter ensembles over a sharded region: each shard runs the members over its calculated cells; the
+// per-(member, catchment) sums combine like the catchment sums
+void ensemble_run(shard_set* s, const double* params, size_t n_members, size_t n_per_set, int start_step, int n_steps,
+                  int collect) {
+    bool any = false;
+    for (char i : s->idle) any = any || !i;
+    if (!any) throw std::runtime_error("ensemble_run: no calculated cells");
+    for_shards(s, [&](size_t k) {
+        if (!s->idle[k])
+            ck(s->r[k], shyft_hip_ensemble_run(s->r[k], params, n_members, n_per_set, start_step, n_steps, collect));
+    });
+    s->ens_members = n_members;
+}
+
+void ensemble_sums(shard_set* s, int series, int area_weighted, size_t step0, size_t n, double* dst, int on_device) {
+    if (s->ens_members == 0) throw std::runtime_error("ensemble_sums: no ensemble run");
+    const size_t P = s->ens_members, C = s->cix_to_cid.size();
+    combine(
+        s, P * C, n,
+        [&](size_t k, double* p) { ck(s->r[k], shyft_hip_ensemble_sums(s->r[k], series, area_weighted, step0, n, p, 1)); },
+        [&](size_t k) {
+            const std::vector<int32_t> rows = catchment_rows(s, k);
+            std::vector<int32_t> m;
+            for (size_t j = 0; j < P; ++j)
+                for (int32_t c : rows) m.push_back(int32_t(j * C) + c);
+            return m;
+        },
+        dst, on_device, true);
+}
+
+double ensemble_last_ms(const shard_set* s) {
+    double m = 0.0;
+    for (size_t k = 0; k < s->S(); ++k)
+        if (!s->idle[k]) m = std::max(m, shyft_hip_ensemble_last_ms(s->r[k]));
+    return m;
+}
+
+shard_set* clone(const shard_set* src) {
+    std::unique_ptr<shard_set, void (*)(shard_set*)> s(new shard_set(), shard_set_destroy);
+    s->stack = src->stack;
+    s->n = src->n;
+    for (size_t k = 0; k < src->S(); ++k) {
+        hip_check(hipSetDevice(src->dev[k]), "hipSetDevice");
+        shyft_hip_region* c = nullptr;
+        if (shyft_hip_region_clone(src->r[k], &c)) throw std::runtime_error(shyft_hip_last_error(nullptr));
+        s->r.push_back(c);
+        hipStream_t st = nullptr;
+        hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        s->streams.push_back(st);
+        s->bufs.emplace_back(new shard_bufs());
+    }
+    s->b = src->b;
+    s->e = src->e;
+    s->dev = src->dev;
+    s->idle = src->idle;
+    s->cix_to_cid = src->cix_to_cid;
+    s->cid_to_cix = src->cid_to_cix;
+    s->child_cids = src->child_cids;
+    s->n_groups = src->n_groups;
+    if (src->path == SHYFT_HIP_COMBINE_RCCL) {
+        s->comms.resize(s->S());
+        nccl_check(ncclCommInitAll(s->comms.data(), int(s->S()), s->dev.data()), "ncclCommInitAll");
+    }
+    s->path = src->path;
+    return s.release();
+}
+
+}  // namespace shards
+}  // namespace shyft_hip_impl

@@ -54,15 +54,37 @@ def _ptr(a: np.ndarray | None):
 
 
 class HipRegion:
-    def __init__(self, stack: int, n_cells: int, device: int = -1):
+    """A region on one device, or -- with `devices` (a list, one entry per shard, repeats allowed) -- one region
+    whose cells are split into len(devices) contiguous shards driven from this process
+    (shyft_hip_region_create_sharded): every method below then works on the whole region."""
+
+    def __init__(self, stack: int, n_cells: int, device: int = -1, devices=None):
         self._L = lib()
         h = C.c_void_p()
-        check(self._L.shyft_hip_region_create(stack, n_cells, device, C.byref(h)), None)
+        if devices is None:
+            check(self._L.shyft_hip_region_create(stack, n_cells, device, C.byref(h)), None)
+        else:
+            d = np.ascontiguousarray(list(devices), dtype=np.int32)
+            check(self._L.shyft_hip_region_create_sharded(stack, n_cells, _ptr(d), d.size, C.byref(h)), None)
         self.h = h
         self.stack = stack
         self.n = n_cells
         self.n_steps = 0
         self.window = 0
+
+    def shards(self) -> list:
+        """[(device, first cell, n_cells)] of every shard ([(device, 0, n)] for an unsharded region)."""
+        dev, c0, nc = C.c_int(), C.c_size_t(), C.c_size_t()
+        S = int(self._L.shyft_hip_region_shards(self.h, 0, None, None, None))
+        out = []
+        for k in range(S):
+            self._L.shyft_hip_region_shards(self.h, k, C.byref(dev), C.byref(c0), C.byref(nc))
+            out.append((dev.value, c0.value, nc.value))
+        return out
+
+    def combine_path(self) -> str:
+        """How shard partial sums are combined: "none" (unsharded), "copy" (shards share a device), "rccl"."""
+        return ("none", "copy", "rccl")[int(self._L.shyft_hip_region_combine_path(self.h))]
 
     def close(self):
         if getattr(self, "h", None):

@@ -1,10 +1,14 @@
 """bench.py's multi-rank path (BASELINE configs[3]/[4] at N>1).
 
-`bench.py --gpus N` without an outside launcher starts N rank processes itself (a parent that never touches
-the GPU), every rank asserts WORLD_SIZE == N, and the per-chunk catchment discharge sums are all-gathered and
+`bench.py --gpus N --launch ranks` without an outside launcher starts N rank processes itself (a parent that never
+touches the GPU), every rank asserts WORLD_SIZE == N, and the per-chunk catchment discharge sums are all-gathered and
 added in rank order (distributed.combine_partials). CPU tests drive that launcher, rendezvous and collective
 with gloo (--dist-check); the GPU tests run the real sharded HipRegion bench with two ranks on one GPU
 (SHYFT_DIST_BACKEND=gloo) and compare the combined catchment sums with a single-rank run of the same region.
+
+The default N > 1 path without a launcher is the engine's (--launch engine): one process, the region in one shard
+per GPU (shyft_hip_region_create_sharded), the partial sums combined inside the engine. On a one-GPU box
+`--gpus 1 --shards K` runs K shards on device 0 through the same code (device-copy combination).
 """
 import json
 import os
@@ -54,7 +58,7 @@ def test_two_ranks_one_gpu_catchment_sums_match_single_rank(stack, tmp_path):
               "--warmup", "0", "--no-cpu-baseline", "--no-routing"]
     p1, o1 = _bench(["--gpus", "1", "--dump-sums", str(tmp_path / "s1.npy")] + common)
     assert p1.returncode == 0, p1.stderr[-2000:]
-    p2, o2 = _bench(["--gpus", "2", "--dump-sums", str(tmp_path / "s2.npy")] + common,
+    p2, o2 = _bench(["--gpus", "2", "--launch", "ranks", "--dump-sums", str(tmp_path / "s2.npy")] + common,
                     env_extra={"SHYFT_DIST_BACKEND": "gloo"})
     assert p2.returncode == 0, p2.stderr[-2000:]
     assert o1["n_gpus"] == 1 and o2["n_gpus"] == 2 and o2["scaling"] == "strong"
@@ -75,7 +79,7 @@ def test_sharded_routing_matches_single_rank(world, cells, tmp_path):
               "3", "--warmup", "0", "--no-cpu-baseline", "--no-catchment-sums"]
     p1, o1 = _bench(["--gpus", "1", "--dump-route", str(tmp_path / "r1.npy")] + common)
     assert p1.returncode == 0, p1.stderr[-2000:]
-    pn, on = _bench(["--gpus", str(world), "--dump-route", str(tmp_path / "rn.npy")] + common,
+    pn, on = _bench(["--gpus", str(world), "--launch", "ranks", "--dump-route", str(tmp_path / "rn.npy")] + common,
                     env_extra={"SHYFT_DIST_BACKEND": "gloo"})
     assert pn.returncode == 0, pn.stderr[-2000:]
     assert o1["n_gpus"] == 1 and on["n_gpus"] == world and "routing" in on
@@ -103,3 +107,25 @@ def test_overlapped_forcing_generation_same_results(tmp_path):
     assert a.shape == (50, 384) and np.isfinite(a).all() and a.sum() > 0
     assert np.array_equal(a, b)
     assert "second window buffer" in o1["config"]["forcing"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stack", ["pt_gs_k", "pt_ss_k"])
+def test_engine_shards_one_process_match_unsharded(stack, tmp_path):
+    """bench's single-process engine path with two shards on device 0: the per-chunk catchment discharge sums and
+    (pt_ss_k) the routed river series equal the unsharded region's bit for bit (the shard boundary, cell 2048, is a
+    catchment boundary; routing groups follow catchments)."""
+    common = ["--stack", stack, "--total-cells", "4096", "--catchments", "100", "--chunk", "48", "--steps", "3",
+              "--warmup", "0", "--no-cpu-baseline"]
+    p1, o1 = _bench(["--gpus", "1", "--dump-sums", str(tmp_path / "s1.npy"), "--dump-route", str(tmp_path / "r1.npy")]
+                    + common)
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    p2, o2 = _bench(["--gpus", "1", "--shards", "2", "--dump-sums", str(tmp_path / "s2.npy"),
+                     "--dump-route", str(tmp_path / "r2.npy")] + common)
+    assert p2.returncode == 0, p2.stderr[-2000:]
+    assert o2["n_gpus"] == 1 and "2 engine shards" in o2["config"]["parallelism"]
+    assert "COPY" in o2["config"]["parallelism"]
+    assert np.array_equal(np.load(tmp_path / "s1.npy"), np.load(tmp_path / "s2.npy"))
+    if stack == "pt_ss_k":
+        r1, r2 = np.load(tmp_path / "r1.npy"), np.load(tmp_path / "r2.npy")
+        assert r1[2].sum() > 0 and np.array_equal(r1, r2)

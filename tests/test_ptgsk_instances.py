@@ -51,10 +51,8 @@ def oracle_run():
 
 @pytest.mark.parametrize("env", [
     {"SHYFT_PTGSK_WAVES": "4"},                           # 256 lanes, 4 waves per SIMD (regions > 131K cells)
-    {"SHYFT_PTGSK_SMALL": "256"},                          # 256 lanes, 2 waves per SIMD
-    {"SHYFT_PTGSK_SMALL": "65"},                           # 64 lanes without the speculative opening
-    {},                                                    # the default small-region instance
-], ids=["w4", "w2-256", "w2-64", "default"])
+    {},                                                    # the default small-region instance (64 lanes, speculative)
+], ids=["w4", "default"])
 def test_instance_bitexact(env, oracle_run, tmp_path):
     out = tmp_path / "g.npz"
     e = dict(os.environ, **env)

@@ -1,0 +1,199 @@
+"""Sharded regions (shyft_hip_region_create_sharded): one region_model whose cells are split into contiguous shards,
+driven from one process -- the engine's multi-GPU path (core/region_model.h:972-1021 runs the whole region in one
+process; catchment sums over all cells, core/cell_model.h:308-333; routing inflows, core/routing.h:344-383).
+
+On a one-GPU box the shards share device 0, so the partial sums combine by device copies; with one shard per GPU the
+same code all-gathers them with RCCL. Per-cell results never depend on the sharding (run_cells has no cross-cell
+coupling): every series and state value must equal the unsharded region's bit for bit. A catchment (or routing
+group) whose cells lie in one shard sums exactly as unsharded (the other shards' partials are +0.0); one that a shard
+boundary cuts is reassociated (within 1e-12 relative)."""
+import numpy as np
+import pytest
+
+from shyft_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+HOUR = synthetic.HOUR_US
+N, C, T = 4096, 100, 96          # cell 2048 starts catchment 51: two shards split at a catchment boundary
+
+
+def _region(stack, devices, n=N, n_catch=C, T_=T, collect=None, state=None):
+    import bench
+    from shyft_amd.region import HipRegion, COLLECT_ALL, STACK_NSTATE
+    sid = {"pt_gs_k": 1, "hbv_stack": 2, "pt_ss_k": 3}[stack]
+    r = HipRegion(sid, n, devices=devices) if devices is not None else HipRegion(sid, n)
+    r.set_geo(synthetic.geo11(n, n_catchments=n_catch))
+    r.set_parameters(bench.stack_defaults(stack, 1)[0])
+    r.set_time_axis(synthetic.T0_2015_US, HOUR, T_)
+    r.set_collection(COLLECT_ALL if collect is None else collect)
+    r.set_state(bench.stack_defaults(stack, n)[1] if state is None else state)
+    return r
+
+
+def _run(r, T_=T):
+    r.synthetic_forcing(synthetic.SEED, 0, T_)
+    r.run_cells(0, 0, T_)
+
+
+def _same(a, b):
+    return np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("stack", ["pt_gs_k", "hbv_stack", "pt_ss_k"])
+def test_two_shards_on_one_device_equal_unsharded(stack):
+    ref, sh = _region(stack, None), _region(stack, [0, 0])
+    try:
+        assert sh.shards() == [(0, 0, N // 2), (0, N // 2, N // 2)]
+        assert sh.combine_path() == "copy" and ref.combine_path() == "none"
+        _run(ref)
+        _run(sh)
+        ns = 9 if stack == "hbv_stack" else 8
+        for k in range(ns):
+            assert _same(sh.get_series(k, 0, T), ref.get_series(k, 0, T)), f"series {k}"
+        assert _same(sh.get_state(), ref.get_state())
+        for v in range(5):
+            assert _same(sh.get_forcing(v, 0, T), ref.get_forcing(v, 0, T))
+        assert np.array_equal(sh.catchment_ids(), ref.catchment_ids())
+        assert _same(sh.catchment_sums(0, 0, T), ref.catchment_sums(0, 0, T))
+        # a selection inside one shard reduces the same cells in the same order: exact; one that spans the shards
+        # adds the shards' partial sums (reassociated)
+        assert _same(sh.statistics(0, [1, 50]), ref.statistics(0, [1, 50]))
+        assert _same(sh.statistics(0, [77, 100], weighted=True), ref.statistics(0, [77, 100], weighted=True))
+        assert np.allclose(sh.statistics(0, [1, 50, 51, 100]), ref.statistics(0, [1, 50, 51, 100]), rtol=1e-12, atol=0)
+        assert np.allclose(sh.statistics(0, [3, 77], weighted=True), ref.statistics(0, [3, 77], weighted=True),
+                           rtol=1e-12, atol=0)
+        from shyft_amd.region import SCOPE_CELL_IX
+        cells = [0, 5, 2047, 2048, 4095]
+        got = sh.statistics(0, cells, scope=SCOPE_CELL_IX)
+        exp = ref.statistics(0, cells, scope=SCOPE_CELL_IX)
+        assert np.allclose(got, exp, rtol=1e-12, atol=0)   # a cut selection: reassociated partial sums
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_three_shards_cut_catchments_within_reassociation():
+    ref, sh = _region("pt_gs_k", None), _region("pt_gs_k", [0, 0, 0])
+    try:
+        _run(ref)
+        _run(sh)
+        assert _same(sh.get_series(0, 0, T), ref.get_series(0, 0, T))
+        a, b = sh.catchment_sums(0, 0, T), ref.catchment_sums(0, 0, T)
+        assert np.allclose(a, b, rtol=1e-12, atol=0)
+        cut = {int(synthetic.geo11(N, n_catchments=C)[c0, 4]) for (_, c0, _) in sh.shards()[1:]}
+        whole = [i for i, cid in enumerate(ref.catchment_ids()) if int(cid) not in cut]
+        assert _same(a[whole], b[whole])                   # catchments inside one shard: exact
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_routing_group_sums_and_routed_river_equal_unsharded():
+    from shyft_amd import api
+    from shyft_amd.region import route
+    ref, sh = _region("pt_ss_k", None), _region("pt_ss_k", [0, 0])
+    try:
+        _, _, group = synthetic.cell_routing(N, C)
+        G = C * len(synthetic.ROUTE_DISTANCES)
+        for r in (ref, sh):
+            r.set_routing_groups(group, G)
+            _run(r)
+        a, b = sh.routing_group_sums(0, T), ref.routing_group_sums(0, T)
+        assert _same(a, b)
+        steps = [int(d / 3600.0 + 0.5) for d in synthetic.ROUTE_DISTANCES]
+        guhg = [api.make_uhg_from_gamma(steps[k], 7.0, 0.0) for _ in range(C) for k in range(len(steps))]
+        rivers = synthetic.river_network(C)
+        ruhg = [api.make_uhg_from_gamma(int((d / v) / 3600.0 + 0.5), al, be) for (_, _, d, v, al, be) in rivers]
+        down = [ds - 1 for (_, ds, *_rest) in rivers]
+        gr = [g // len(steps) for g in range(G)]
+        out_a = route(a, guhg, gr, ruhg, down)
+        out_b = route(b, guhg, gr, ruhg, down)
+        for x, y in zip(out_a, out_b):
+            assert _same(x, y)
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_catchment_filter_idle_shard_and_interpolation():
+    """A filter on catchments of the second shard only: the first shard is idle (not run, not interpolated); the
+    calculated cells match the unsharded filtered region, the IDW forcing too (per-cell neighbour tables)."""
+    import bench
+    from tests.test_idw_c3 import C3_PARAMS
+    ref, sh = _region("pt_gs_k", None), _region("pt_gs_k", [0, 0])
+    try:
+        xyz = bench.station_network(N)
+        vals = bench.station_values(xyz, 0, T)
+        for r in (ref, sh):
+            r.set_catchment_filter([60, 61, 99])
+            for v in range(5):
+                r.interpolate(v, xyz, vals[v], 0, C3_PARAMS[v])
+            r.run_cells(0, 0, T)
+        cid = synthetic.geo11(N, n_catchments=C)[:, 4]
+        on = np.isin(cid, [60, 61, 99])
+        for v in range(5):
+            a, b = sh.get_forcing(v, 0, T), ref.get_forcing(v, 0, T)
+            assert _same(a[:, on], b[:, on])
+        assert _same(sh.get_series(0, 0, T)[:, on], ref.get_series(0, 0, T)[:, on])
+        assert _same(sh.catchment_sums(0, 0, T), ref.catchment_sums(0, 0, T))
+        assert sh.interpolation_path(0) == ref.interpolation_path(0)
+        with pytest.raises(RuntimeError, match="no cells have supplied cid"):
+            sh.set_catchment_filter([12345])
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_ensemble_and_host_roundtrips():
+    from shyft_amd.region import COLLECT_DISCHARGE
+    import bench
+    ref, sh = _region("pt_gs_k", None), _region("pt_gs_k", [0, 0])
+    try:
+        rng = np.random.default_rng(1)
+        f = rng.uniform(0, 1, size=(T, N))
+        for r in (ref, sh):
+            _run(r)
+            r.set_forcing(1, 0, f)          # host forcing split over the shards and back
+        assert _same(sh.get_forcing(1, 0, T), f)
+        p = np.tile(bench.stack_defaults("pt_gs_k", 1)[0], (3, 1))
+        p[1, 0] -= 0.3                      # kirchner c1 of member 1
+        ref.ensemble_run(p, 0, T, COLLECT_DISCHARGE)
+        sh.ensemble_run(p, 0, T, COLLECT_DISCHARGE)
+        assert _same(sh.ensemble_sums(0, 0, T), ref.ensemble_sums(0, 0, T))
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_api_model_with_devices():
+    """PTGSKModel(..., devices=[0, 0]) behaves as the unsharded model through the reference's Python scenario
+    (test_region_model_stacks.py:114-200: interpolate from a region environment, run_cells, the discharge
+    statistics) and a deep clone (create_opt_model_clone) of it stays sharded."""
+    from shyft_amd import api
+    from shyft_amd.api import pt_gs_k
+    from tests.test_api_region_model import build_model, dummy_env, interpolation_parameter
+
+    def sharded(gcds, p):
+        return pt_gs_k.PTGSKModel(gcds, p, devices=[0, 0])
+
+    a = build_model(pt_gs_k.PTGSKModel, pt_gs_k.PTGSKParameter, 20, num_catchments=4)
+    b = build_model(sharded, pt_gs_k.PTGSKParameter, 20, num_catchments=4)
+    assert list(b.shard_devices) == [0, 0] and list(a.shard_devices) == [0]
+    cal = api.Calendar()
+    ta = api.TimeAxisFixedDeltaT(cal.time(2015, 1, 1, 0, 0, 0), api.deltahours(1), 240)
+    for m in (a, b):
+        m.initialize_cell_environment(ta)
+        m.interpolate(interpolation_parameter(), dummy_env(ta, m.get_cells()[10].geo.mid_point()))
+        m.set_state_collection(-1, True)
+        m.run_cells()
+    for cids in ([], [1], [2, 4]):
+        qa = a.statistics.discharge(api.IntVector(cids))
+        qb = b.statistics.discharge(api.IntVector(cids))
+        assert np.allclose(qa.values.to_numpy(), qb.values.to_numpy(), rtol=1e-12, atol=0)  # cids interleave (i % 4)
+    ea = a.statistics.charge(api.IntVector([1, 2, 17]), ix_type=api.stat_scope.cell).values.to_numpy()
+    eb = b.statistics.charge(api.IntVector([1, 2, 17]), ix_type=api.stat_scope.cell).values.to_numpy()
+    assert np.allclose(ea, eb, rtol=1e-12, atol=0)
+    c = pt_gs_k.create_opt_model_clone(b)
+    assert list(c.shard_devices) == [0, 0]
+    c.run_cells()

@@ -9,7 +9,7 @@ others=$(ls _obj/*.o _obj/kernels/*.o | grep -v "kernels/ptgsk.o")
 while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2
   (/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $flags -c kernels/ptgsk.hip -o /tmp/ptgsk_$name.o &&
-   /opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o ../../tools/variants/$name.so $others /tmp/ptgsk_$name.o -lrocblas &&
+   /opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o ../../tools/variants/$name.so $others /tmp/ptgsk_$name.o -lrocblas -lrccl &&
    echo built $name) &
 done
 wait
