@@ -43,7 +43,9 @@ constexpr int WAVES_PERLANE = 2;  // the per-lane-parameter launch (catchment pa
 // those paths and their
 // pointers are compiled out, which keeps the step loop's scalar registers (the uniform parameter row, the series
 // bases) within the SGPR file instead of spilled to VGPR lanes (a v_readlane_b32, VALU issue, per use)
-template <bool UNIFORM, int NB, bool LEAN = false>
+// EXACT: the parameter set has exactly NB bins (the reference's default distribution has 5): the bin count is a
+// compile-time constant, so every "i < nb" guard of the bin loops (and the selects it feeds) folds away
+template <bool UNIFORM, int NB, bool LEAN = false, bool EXACT = false>
 __global__ __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(UNIFORM ? SHYFT_HBV_WAVES : WAVES_PERLANE, UNIFORM ? SHYFT_HBV_WAVES : WAVES_PERLANE)))
 void hbv_run_kernel(const hbv_kargs a) {
@@ -56,7 +58,7 @@ void hbv_run_kernel(const hbv_kargs a) {
     const size_t fcl = !LEAN && a.fcol ? (size_t)a.fcol[cell] : (size_t)cell;
     const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * HBV_NP;
     hbv_snow_par_t<NB> sp_par;
-    sp_par.nb = (int)P[HK_NB];
+    sp_par.nb = EXACT ? NB : (int)P[HK_NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         sp_par.s[i] = P[HK_S0 + i];
@@ -235,7 +237,9 @@ void hbv_run_kernel(const hbv_kargs a) {
 hipError_t launch_hbv_run(const hbv_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (a.uniform_params && a.nb_max <= 5 && !a.state_series && !a.fcol && a.collect == 0)
+    if (a.uniform_params && a.nb_max == 5 && !a.state_series && !a.fcol && a.collect == 0)
+        hipLaunchKernelGGL((hbv_run_kernel<true, 5, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.uniform_params && a.nb_max <= 5 && !a.state_series && !a.fcol && a.collect == 0)
         hipLaunchKernelGGL((hbv_run_kernel<true, 5, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
         hipLaunchKernelGGL((hbv_run_kernel<true, 5>), dim3(grid), dim3(BLOCK), 0, stream, a);

@@ -33,7 +33,8 @@ constexpr int WAVES_UNIFORM = 4;  // the uniform-parameter instance; measured (5
 // UNIFORM: every cell uses parameter set 0 (the row, incl. the bin distribution, in SGPRs instead of VGPRs).
 // NB: register capacity of the snow bins, HBV_MAX_BINS or 5 (as in the hbv_stack kernel: one parameter set of at
 // most 5 bins and no state series; bins NB..7 of the state are written as 0, the oracle's padding).
-template <bool UNIFORM, int NB>
+// EXACT: the parameter set has exactly NB bins: the bin count is a compile-time constant (hbv_stack's kernel)
+template <bool UNIFORM, int NB, bool EXACT = false>
 __global__ __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(UNIFORM ? WAVES_UNIFORM : SHYFT_PTHSK_WAVES, UNIFORM ? WAVES_UNIFORM : SHYFT_PTHSK_WAVES)))
 void pthsk_run_kernel(const pthsk_kargs a) {
@@ -47,7 +48,7 @@ void pthsk_run_kernel(const pthsk_kargs a) {
     const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[cell] * PTHSK_NP;
 
     hbv_snow_par_t<NB> sp_par;
-    sp_par.nb = (int)P[PH_NB];
+    sp_par.nb = EXACT ? NB : (int)P[PH_NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         sp_par.s[i] = P[PH_S0 + i];
@@ -183,7 +184,9 @@ void pthsk_run_kernel(const pthsk_kargs a) {
 hipError_t launch_pthsk_run(const pthsk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
-    if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
+    if (a.uniform_params && a.nb_max == 5 && !a.state_series)
+        hipLaunchKernelGGL((pthsk_run_kernel<true, 5, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.uniform_params && a.nb_max <= 5 && !a.state_series)
         hipLaunchKernelGGL((pthsk_run_kernel<true, 5>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.uniform_params)
         hipLaunchKernelGGL((pthsk_run_kernel<true, HBV_MAX_BINS>), dim3(grid), dim3(BLOCK), 0, stream, a);

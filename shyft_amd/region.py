@@ -158,6 +158,10 @@ class HipRegion:
         self._chk(self._L.shyft_hip_get_forcing(self.h, var, step0, n, _ptr(out), 0))
         return out
 
+    def get_forcing_device(self, var: int, step0: int, n: int, dev_ptr: int):
+        """[n][cells] forcing rows into device memory (e.g. a torch tensor's data_ptr())."""
+        self._chk(self._L.shyft_hip_get_forcing(self.h, var, step0, n, C.c_void_p(dev_ptr), 1))
+
     def interpolate(self, var: int, src_xyz: np.ndarray, src_values: np.ndarray, step0: int, idw_param):
         """IDW of one forcing variable from sources (src_values [n][S] on the model axis)."""
         xyz = np.ascontiguousarray(src_xyz, dtype=np.float64).reshape(-1, 3)

@@ -270,3 +270,63 @@ def test_c3_chain_idw_then_pt_gs_k_bitexact():
     ok, msg = _same(got, exp["full"])
     assert ok, "series: " + msg
     assert np.array_equal(st, exp["state"])
+
+
+@pytest.mark.gpu
+def test_c3_fullsize_1m_cells_two_windows_sampled_bitexact():
+    """configs[2] at full size: 1,048,576 cells, the bench's 500-station network, two 438-step windows (the bench's
+    chunks) of run_interpolation (all five variables, asserted on the wavefront-union gather) then run_cells with the
+    state carried in HBM; 512 sampled cells (first and last included) compared bit for bit with the oracle's IDW on
+    just those cells (all 500 stations) and the oracle's pt_gs_k run over the same 876 steps."""
+    import torch
+    import bench
+    from shyft_amd import synthetic
+    from shyft_amd.region import HipRegion, PT_GS_K, COLLECT_ALL
+    from tests import oracle_lib
+    N, W = 1 << 20, 438
+    T = 2 * W
+    geo = synthetic.geo11(N)
+    xyz = bench.station_network(N)
+    vals = bench.station_values(xyz, 0, T)                            # [5][T][500]
+    rng = np.random.default_rng(19)
+    vals = np.where((rng.uniform(size=vals.shape) < 0.01) & (rng.uniform(size=(1, T, 1)) < 0.2), np.nan, vals)
+    idx = np.unique(np.concatenate([[0, N - 1], rng.choice(N, 510, replace=False)]))
+    p = synthetic.default_ptgsk_parameters()
+    dev = torch.device("cuda", 0)
+    got = np.empty((8, T, idx.size))
+    got_f = np.empty((5, T, idx.size))
+    r = HipRegion(PT_GS_K, N, device=0)
+    try:
+        r.set_geo(geo)
+        r.set_parameters(p)
+        r.set_time_axis(synthetic.T0_2015_US, HOUR, T, W)
+        r.set_collection(COLLECT_ALL)
+        r.set_state(synthetic.default_ptgsk_state(N))
+        buf = torch.empty((W, N), dtype=torch.float64, device=dev)
+        cols = torch.from_numpy(idx).to(dev)
+        for w0 in (0, W):
+            r.move_window(w0, 0)
+            for var in range(5):
+                r.interpolate(var, xyz, np.ascontiguousarray(vals[var, w0:w0 + W]), w0, C3_PARAMS[var])
+                assert r.interpolation_path(var) == "wave", f"variable {var}: {r.interpolation_path(var)}"
+            r.run_cells(0, w0, W)
+            for var in range(5):
+                torch.cuda.synchronize(dev)
+                r.get_forcing_device(var, w0, W, buf.data_ptr())
+                got_f[var, w0:w0 + W] = buf.index_select(1, cols).cpu().numpy()
+            for k in range(8):
+                torch.cuda.synchronize(dev)
+                r.get_series_device(k, w0, W, buf.data_ptr())
+                got[k, w0:w0 + W] = buf.index_select(1, cols).cpu().numpy()
+        state = r.get_state()[idx]
+    finally:
+        r.close()
+    exp_f = np.stack([oracle_idw(IDW_PARAMS[v][0], xyz, np.ascontiguousarray(vals[v]), geo[idx, :3], C3_PARAMS[v],
+                                 dst_slope=geo[idx, 5]) for v in range(5)])
+    ok, msg = _same(got_f, exp_f)
+    assert ok, "forcing: " + msg
+    exp = oracle_lib.ptgsk_run(geo[idx], p, synthetic.default_ptgsk_state(idx.size), synthetic.T0_2015_US, HOUR, exp_f,
+                               full=True, ncore=8)
+    ok, msg = _same(got, exp["full"])
+    assert ok, "series: " + msg
+    assert np.array_equal(state, exp["state"])
