@@ -26,12 +26,25 @@ struct gs_state {
 };
 
 // dlgamma(shape) cache: shape (the SDC alpha state) changes only on snowfall,
-// melt or reset, so most calls of calc_snow_state within a cell reuse it.
+// melt or reset, so most calls of calc_snow_state within a cell reuse it. The functions below take any cache
+// type with this get(): the kernel keeps the cache in its lane's LDS slots (lgamma_cache_lds) rather than in
+// registers that the step loop would spill around every call.
 struct lgamma_cache {
     double a = -1.0, v = 0.0;
     __device__ inline double get(double shape) {
         if (shape != a) { a = shape; v = dlgamma(shape); }
         return v;
+    }
+};
+// a[threadIdx.x], v[threadIdx.x] of two workgroup arrays (the slot address is formed from threadIdx.x at each
+// use, not held in a register)
+struct lgamma_cache_lds {
+    double* a;
+    double* v;
+    __device__ inline double get(double shape) {
+        const int t = threadIdx.x;
+        if (shape != a[t]) { a[t] = shape; v[t] = dlgamma(shape); }
+        return v[t];
     }
 };
 
@@ -43,9 +56,10 @@ struct gs_lw {
 };
 
 // gamma_snow.h:230-260
+template <class LGC>
 __device__ inline void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
                                        double max_water_frac, double temp_swe, double& swe, double& sca,
-                                       lgamma_cache& lgc, gs_lw& lw) {
+                                       LGC& lgc, gs_lw& lw) {
     lw.p = lw.p1 = __builtin_nan("");
     double y = 0.0, y1 = 0.0;
     const double m = shape * scale;
@@ -181,8 +195,7 @@ struct gs_cell {
 // evaluates them).
 struct gs_mid {
     bool done;  // the early "no snow" path was taken (gamma_snow.h:313-322)
-    bool need;  // corr_lwc job: z1, a1, b1, a2, b2 (+ q1 = calc_q(a1, b1, z1) or NaN, lga2 = lgamma(a2))
-    double z1, a1, b1, a2, b2, q1, lga2;
+    bool need;  // a corr_lwc job was handed to the caller's enqueue
     double prec, snow, rain, albedo, lwc, surface_heat, alpha, temp_swe, sca, storage, sdc_melt_mean, acc_melt,
         iso_pot_energy, potential_melt, start_storage, sdc_scale;
 };
@@ -198,10 +211,14 @@ struct gs_carry {
     bool ok = false;
 };
 
+// enqueue(z1, a1, b1, a2, b2, q1, lga2) receives the step's corr_lwc job where it arises (q1 = calc_q(a1, b1, z1)
+// or NaN, lga2 = lgamma(a2)): the kernel writes it straight into its workgroup's LDS job queue, so the seven job
+// values are not held in registers (or scratch) until a later queue pass
+template <class LGC, class Enqueue>
 __device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
                                       const double* __restrict__ P, const gs_cell& cc, double T, double rad,
-                                      double prec_mm_h, double wind_speed, double rel_hum, lgamma_cache& lgc,
-                                      const gs_carry& carry) {
+                                      double prec_mm_h, double wind_speed, double rel_hum, LGC& lgc,
+                                      const gs_carry& carry, Enqueue&& enqueue) {
     m.need = false;
     m.done = false;
     double sdc_melt_mean = s.sdc_melt_mean;
@@ -290,16 +307,14 @@ __device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, d
             if (lwc > 0.0 && sdc_snow > 0.01 * sdc_melt_mean) {
                 // z1_guess (gamma_snow.h:427-430) is computed by the reference but unused by corr_lwc
                 m.need = true;
-                m.z1 = lwc / max_water;
-                m.a1 = alpha_prev;
-                m.b1 = sdc_scale_prev > 0.0 ? sdc_scale_prev : sdc_scale;
-                m.a2 = alpha;
-                m.b2 = sdc_scale;
+                const double z1 = lwc / max_water;
+                const double a1 = alpha_prev;
+                const double b1 = sdc_scale_prev > 0.0 ? sdc_scale_prev : sdc_scale;
                 // calc_q(a1, b1, z1) = a1 b1 P(a1+1, z1/b1) + z1 (1 - P(a1, z1/b1)) (gamma_snow.h:209-212) from the
                 // opening calc_snow_state's liquid-water pair (same shape, scale and point, z1 / b1 = sat / scale)
-                m.q1 = (sdc_scale_prev > 0.0 && lw.p == lw.p) ? m.a1 * m.b1 * lw.p1 + m.z1 * (1.0 - lw.p)
-                                                               : __builtin_nan("");
-                m.lga2 = lgc.get(alpha);
+                const double q1 = (sdc_scale_prev > 0.0 && lw.p == lw.p) ? a1 * b1 * lw.p1 + z1 * (1.0 - lw.p)
+                                                                          : __builtin_nan("");
+                enqueue(z1, a1, b1, alpha, sdc_scale, q1, lgc.get(alpha));
             }
         }
     }
@@ -318,9 +333,10 @@ __device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, d
     m.sdc_scale = sdc_scale;
 }
 
+template <class LGC>
 __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r_sca, double& r_storage,
                                      double& r_outflow, bool snow_season, double dt_us, const double* __restrict__ P,
-                                     const gs_cell& cc, double prec_mm_h, lgamma_cache& lgc, gs_carry& carry) {
+                                     const gs_cell& cc, double prec_mm_h, LGC& lgc, gs_carry& carry) {
     if (m.done) {
         carry.ok = false;
         s.albedo = P[PK_MAX_ALBEDO];
@@ -340,11 +356,12 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
     double sdc_melt_mean = m.sdc_melt_mean, acc_melt = m.acc_melt, potential_melt = m.potential_melt;
     double sdc_scale = m.sdc_scale;
     if (acc_melt < 0.0) {
-        if (m.need) {
-            lwc = z * max_water;
-            gs_lw lw2;
-            calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc, lw2);
-        }
+        // the reference follows corr_lwc with calc_snow_state(alpha, sdc_scale, ..., lwc, ..., storage, sca)
+        // (gamma_snow.h:433-434), whose two outputs are dead: this branch only overwrites storage and sca (or
+        // leaves them alone) before the step's final calc_snow_state assigns both (gamma_snow.h:472, below), and
+        // calc_snow_state reads neither. Skipping it changes no bit of the step (its incomplete-gamma evaluation,
+        // run by every wavefront holding a job lane, was ~6 % of the kernel's static code).
+        if (m.need) lwc = z * max_water;
         lwc += rain;
         if (sdc_melt_mean <= potential_melt) {
             storage = 0.0;
@@ -406,15 +423,6 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
     r_sca = sca;
     r_storage = storage;
     r_outflow = (outflow * 3600000000.0) / dt_us;
-}
-
-__device__ inline double gs_solve_lwc(const gs_mid& m) {
-#ifdef SHYFT_PROF
-    int nf = 0;
-    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2, m.q1, m.lga2, nf);
-#else
-    return gs_corr_lwc(m.z1, m.a1, m.b1, m.a2, m.b2, m.q1, m.lga2);
-#endif
 }
 
 // ------------------------------------------------------------------ kirchner

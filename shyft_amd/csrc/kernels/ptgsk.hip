@@ -69,10 +69,10 @@ constexpr int BRENT_PRIO = 3;
 // B: cells (lanes) per workgroup. SPEC: the speculative Brent opening (device/gs_brent.h), for small regions.
 template <bool COMPACT, bool UNIFORM, bool ENS = false, int WAVES = SHYFT_LB_WAVES, int B = BLOCK, bool SPEC = false>
 __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a) {
+    static_assert(COMPACT, "the Brent jobs always go through the workgroup queue");
     const int cell = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = cell < a.n_cells;
     if (valid && a.active && !a.active[cell]) valid = false;
-    if (!COMPACT && !valid) return;
     const int lc = valid ? cell : 0;  // out-of-range lanes of a COMPACT block read cell 0 and store nothing
     const size_t N = (size_t)a.n_cells;
     const size_t NF = ENS ? (size_t)a.f_cols : N;
@@ -88,7 +88,9 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     gcell.inv_cv2 = cc[PC_INV_CV2 * N + lc];
     // the cell constants live in LDS, not in VGPRs: each use reloads its lane's slot (the barriers of the
     // step keep the compiler from hoisting the loads), so none of them is live across the Brent phase
-    __shared__ double lcc[11][B];
+    // rows 0-9: the cell constants; rows 10-11: the lane's lgamma cache (shape, value), so that every per-lane LDS
+    // slot is one address register plus an immediate offset
+    __shared__ double lcc[12][B];
     {
         const int t = threadIdx.x;
         lcc[0][t] = gcell.forest_fraction;
@@ -101,7 +103,6 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         lcc[7][t] = cc[PC_DIRECT_RESPONSE * N + lc];
         lcc[8][t] = cc[PC_KIRCHNER_FRACTION * N + lc];
         lcc[9][t] = cc[PC_AREA * N + lc];
-        lcc[10][t] = cc[PC_GLACIER_AREA * N + lc];
     }
 #define glacier_fraction (lcc[4][threadIdx.x])
 #define snow_storage_fraction (lcc[5][threadIdx.x])
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
 #define direct_response_fraction (lcc[7][threadIdx.x])
 #define kirchner_fraction (lcc[8][threadIdx.x])
 #define cell_area_m2 (lcc[9][threadIdx.x])
-#define glacier_area_m2 (lcc[10][threadIdx.x])
+#define glacier_area_m2 (lcc[9][threadIdx.x] * lcc[4][threadIdx.x])  // PC_GLACIER_AREA = area * glacier (region.hip)
 #define LOAD_GCELL()                                   \
     do {                                               \
         gcell.forest_fraction = lcc[0][threadIdx.x];   \
@@ -132,7 +133,9 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     s.iso_pot_energy = st[PS_ISO_POT_ENERGY * N + lc];
     s.temp_swe = st[PS_TEMP_SWE * N + lc];
     double q = st[PS_KIRCHNER_Q * N + lc];
-    lgamma_cache lgc;
+    lcc[10][threadIdx.x] = -1.0;  // the lgamma cache (device/ptgsk_dev.h)
+    lcc[11][threadIdx.x] = 0.0;
+    lgamma_cache_lds lgc{lcc[10], lcc[11]};
     gs_carry carry;
     int32_t err = 0;
 
@@ -151,7 +154,9 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
 
     // Brent job queue of the workgroup (COMPACT)
-    __shared__ double jz1[B], ja1[B], jb1[B], ja2[B], jb2[B], jq1[B], jlg2[B], jres[B];
+    // (jres aliases jz1: a solving lane reads its job's z1 before it writes the job's result into the same slot)
+    __shared__ double jz1[B], ja1[B], jb1[B], ja2[B], jb2[B], jq1[B], jlg2[B];
+    double* const jres = jz1;
     __shared__ double jsz[SPEC ? 64 : 1], jsf[SPEC ? 64 : 1];  // speculative opening: point and f of lane t
     __shared__ int jcount[2];
     if (COMPACT) {
@@ -200,20 +205,21 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         m.need = false;
         m.done = true;
         LOAD_GCELL();
+        if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (race-free: see DESIGN.md)
+        int slot = -1;
+        // the step's Brent job goes into the queue where gs_front forms it
+        auto enqueue = [&](double z1, double a1, double b1, double a2, double b2, double q1, double lga2) {
+            slot = atomicAdd(&jcount[i & 1], 1);
+            jz1[slot] = z1; ja1[slot] = a1; jb1[slot] = b1; ja2[slot] = a2; jb2[slot] = b2;
+            jq1[slot] = q1; jlg2[slot] = lga2;
+        };
 #ifndef SHYFT_ABLATE_SNOW
         if (valid)
-            gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc, carry);
+            gs_front(s, m, start_melt, a.dt_s, a.dt_us, P, gcell, temp, rad, prec, wind_speed, rel_hum, lgc, carry, enqueue);
 #endif
         PROF_MARK(0);  // forcing + gs_front
         double z = 0.0;
-        if (COMPACT) {
-            if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (race-free: see DESIGN.md)
-            int slot = -1;
-            if (m.need) {
-                slot = atomicAdd(&jcount[i & 1], 1);
-                jz1[slot] = m.z1; ja1[slot] = m.a1; jb1[slot] = m.b1; ja2[slot] = m.a2; jb2[slot] = m.b2;
-                jq1[slot] = m.q1; jlg2[slot] = m.lga2;
-            }
+        {
             __syncthreads();
             PROF_MARK(1);  // job queue + barrier
             const int nj = jcount[i & 1];
@@ -269,8 +275,6 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                 __syncthreads();
                 if (slot >= 0) z = jres[slot];
             }
-        } else if (m.need) {
-            z = gs_solve_lwc(m);
         }
         PROF_MARK(2);  // Brent phase
         if (!valid) continue;
@@ -357,8 +361,12 @@ __global__ __launch_bounds__(256, 8) void ptgsk_callee_budget_kernel(const ptgsk
     gs_carry carry;
     gs_cell gc{};
     double q = a.dt_s, qa = 0.0, sca, sto, outf;
-    gs_front(s, m, c == 0, a.dt_s, a.dt_us, a.params, gc, q, q, q, q, q, lgc, carry);
-    const double z = gs_corr_lwc_lean(m.z1, m.a1, m.b1, m.a2, m.b2, m.q1, m.lga2);
+    double j[7] = {};
+    gs_front(s, m, c == 0, a.dt_s, a.dt_us, a.params, gc, q, q, q, q, q, lgc, carry,
+             [&](double z1, double a1, double b1, double a2, double b2, double q1, double lga2) {
+                 j[0] = z1; j[1] = a1; j[2] = b1; j[3] = a2; j[4] = b2; j[5] = q1; j[6] = lga2;
+             });
+    const double z = gs_corr_lwc_lean(j[0], j[1], j[2], j[3], j[4], j[5], j[6]);
     gs_back(s, m, z, sca, sto, outf, c == 1, a.dt_us, a.params, gc, q, lgc, carry);
     double e;
     const double pe = pt_pot_evap_exp(0.2, 1.26, q, q, q, q, e);
