@@ -424,25 +424,15 @@ __global__ __launch_bounds__(64) void idw_wave_union_kernel(idw_union_args a) {
     }
 }
 
-#ifndef SHYFT_IDW_TW
-#define SHYFT_IDW_TW 1
-#endif
-#ifndef SHYFT_IDW_WDZ
-#define SHYFT_IDW_WDZ 1
-#endif
 template <int KT, int KIND, bool BYEQ>
-__global__ __launch_bounds__(256, SHYFT_IDW_TW) void idw_wave_gather_kernel(idw_gather_args a) {
+__global__ __launch_bounds__(256) void idw_wave_gather_kernel(idw_gather_args a) {
+    constexpr int P = 4;  // source rows in flight per lane
     constexpr bool TEMP = KIND == IDW_TEMPERATURE;
-    // G rows go through one neighbour pass for the temperature gather (pairs: 5.33 -> 5.25 ms per 730-row chunk, 1M
+    // row pairs through one neighbour pass for the temperature gather (5.33 -> 5.25 ms per 730-row chunk, 1M
     // cells, vs 6.20 single-row); the 20-member precipitation pass measured slower with pairs (more VGPRs, 3 -> 2
-    // waves per SIMD), so the other kinds load rows in pairs but sum them one at a time
-#ifndef SHYFT_IDW_TG
-#define SHYFT_IDW_TG 2
-#endif
-    constexpr int G = TEMP ? SHYFT_IDW_TG : 2;
-    constexpr bool FUSE = TEMP;
-    constexpr int P = 2 * G;  // source rows in flight per lane
-    __shared__ double vslot[4][2 * G][64];             // each wavefront's union values of a row group (double-buffered)
+    // waves per SIMD), so it keeps single rows
+    constexpr bool PAIR = TEMP;
+    __shared__ double vslot[4][4][64];                 // each wavefront's union values of a row pair (double-buffered)
     __shared__ double zslot[TEMP ? 4 : 1][64];         // the union's z
     __shared__ double xslot[BYEQ ? 4 : 1][64], yslot[BYEQ ? 4 : 1][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -469,14 +459,12 @@ __global__ __launch_bounds__(256, SHYFT_IDW_TW) void idw_wave_gather_kernel(idw_
     for (int q = 0; q < (KT + 3) / 4; ++q) lw[q] = 4 * q < kept ? a.lidx[(size_t)q * N + j] : 0u;
     auto L = [&](int k) { return (int)((lw[k >> 2] >> (8 * (k & 3))) & 0xffu); };
     double nw[KT];
-    // temperature: d.z - s.z of each neighbour held in registers (WDZ) or formed from the union's z in LDS per use
-    constexpr bool WDZ = TEMP && DZREG && !BYEQ && SHYFT_IDW_WDZ;
-    double naux[KIND == IDW_PRECIPITATION || WDZ ? KT : 1];
+    double naux[KIND == IDW_PRECIPITATION || (TEMP && DZREG && !BYEQ) ? KT : 1];
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
         const bool in = k < kept;
         nw[k] = in ? a.w[k * N + j] : 0.0;
-        if (KIND == IDW_PRECIPITATION || WDZ) naux[k] = in ? a.aux[k * N + j] : 0.0;
+        if (KIND == IDW_PRECIPITATION || (TEMP && DZREG && !BYEQ)) naux[k] = in ? a.aux[k * N + j] : 0.0;
     }
     const double* zs = zslot[TEMP ? wv : 0];
     const double* xs = xslot[BYEQ ? wv : 0];
@@ -619,9 +607,8 @@ __global__ __launch_bounds__(256, SHYFT_IDW_TW) void idw_wave_gather_kernel(idw_
         return scale;
     };
     // neighbour k's transformed value (inverse_distance.h:390-472)
-    auto dz_of = [&](int k, int l) -> double { return WDZ ? naux[k] : dst_z - zs[l]; };
     auto transform = [&](double v, double scale, int k, int l) -> double {
-        if (TEMP) return v + scale * dz_of(k, l);
+        if (TEMP) return v + scale * (DZREG && !BYEQ ? naux[k] : dst_z - zs[l]);
         if (KIND == IDW_PRECIPITATION) return v * naux[k];
         if (KIND == IDW_RADIATION) return v * slope;
         return v;
@@ -652,66 +639,52 @@ __global__ __launch_bounds__(256, SHYFT_IDW_TW) void idw_wave_gather_kernel(idw_
         }
         if (lane_on) out[(size_t)r * N + j] = sum_weight_value / sum_weights;
     };
-    // Rows go in groups of G: the group's values into the wavefront's slots, then -- when every lane of the
-    // wavefront has its KT neighbours and every row of the group is finite -- one pass over the neighbours feeds G
-    // independent sums (each in the reference's order: the same bits as G single-row passes), so one neighbour-slot
-    // decode and one weight register serve G rows and the G add chains overlap.
-    for (int r = 0; r < R; r += G) {
-        const int cnt = R - r < G ? R - r : G;
-        double v[G];
+    // Rows go in pairs: both rows' values into the wavefront's slots, then -- when every lane of the wavefront has
+    // its KT neighbours and both rows are finite -- one pass over the neighbours feeds two independent sums (each
+    // in the reference's order: the same bits as two single-row passes), so one neighbour-slot decode and one
+    // weight register serve two rows and the two add chains overlap.
+    for (int r = 0; r < R; r += 2) {
+        const bool two = r + 1 < R;
+        const double v0 = pv[0], v1 = pv[1];
 #pragma unroll
-        for (int g = 0; g < G; ++g) v[g] = pv[g];
-#pragma unroll
-        for (int p = 0; p + G < P; ++p) pv[p] = pv[p + G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) pv[P - G + g] = (lane < un && r + P - G + g < R) ? src[(size_t)(r + P - G + g) * S + su] : 0.0;
-        double* rows = vslot[wv][((r / G) & 1) * G];
-        bool fin[G];
-        bool all_fin = true;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            rows[g * 64 + lane] = v[g];
-            fin[g] = g >= cnt || __ballot(lane < un && !__builtin_isfinite(v[g])) == 0ull;
-            all_fin = all_fin && fin[g];
-        }
+        for (int p = 0; p + 2 < P; ++p) pv[p] = pv[p + 2];
+        pv[P - 2] = (lane < un && r + P < R) ? src[(size_t)(r + P) * S + su] : 0.0;
+        pv[P - 1] = (lane < un && r + P + 1 < R) ? src[(size_t)(r + P + 1) * S + su] : 0.0;
+        double* row0 = vslot[wv][((r >> 1) & 1) * 2];
+        double* row1 = row0 + 64;
+        row0[lane] = v0;
+        row1[lane] = v1;
+        const bool fin0 = __ballot(lane < un && !__builtin_isfinite(v0)) == 0ull;
+        const bool fin1 = !two || __ballot(lane < un && !__builtin_isfinite(v1)) == 0ull;
         __builtin_amdgcn_wave_barrier();
-        if (FUSE && full && all_fin && cnt == G) {
-            double scale[G], sg[G];
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                scale[g] = row_scale(rows + g * 64, true);
-                sg[g] = 0.0;
-            }
+        if (PAIR && full && fin0 && fin1 && two) {
+            const double scale0 = row_scale(row0, true), scale1 = row_scale(row1, true);
+            double s0 = 0.0, s1 = 0.0;
 #pragma unroll
             for (int k = 0; k < KT; ++k) {
                 const int l = L(k);
-                const double dz = dz_of(k, l);  // (temperature only)
-#pragma unroll
-                for (int g = 0; g < G; ++g) sg[g] += nw[k] * (TEMP ? rows[g * 64 + l] + scale[g] * dz : transform(rows[g * 64 + l], scale[g], k, l));
+                s0 += nw[k] * transform(row0[l], scale0, k, l);
+                s1 += nw[k] * transform(row1[l], scale1, k, l);
             }
             if (lane_on) {
-#pragma unroll
-                for (int g = 0; g < G; ++g) out[(size_t)(r + g) * N + j] = sg[g] / sw_all;
+                out[(size_t)r * N + j] = s0 / sw_all;
+                out[(size_t)(r + 1) * N + j] = s1 / sw_all;
             }
             continue;
         }
+        if (full && fin0) {  // the single-row straight-line sum
+            const double scale0 = row_scale(row0, true);
+            double s0 = 0.0;
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            if (g >= cnt) break;
-            const double* row = rows + g * 64;
-            if (full && fin[g]) {  // the single-row straight-line sum
-                const double scale0 = row_scale(row, true);
-                double s0 = 0.0;
-#pragma unroll
-                for (int k = 0; k < KT; ++k) {
-                    const int l = L(k);
-                    s0 += nw[k] * transform(row[l], scale0, k, l);
-                }
-                if (lane_on) out[(size_t)(r + g) * N + j] = s0 / sw_all;
-            } else {
-                one_row(r + g, row, fin[g]);
+            for (int k = 0; k < KT; ++k) {
+                const int l = L(k);
+                s0 += nw[k] * transform(row0[l], scale0, k, l);
             }
+            if (lane_on) out[(size_t)r * N + j] = s0 / sw_all;
+        } else {
+            one_row(r, row0, fin0);
         }
+        if (two) one_row(r + 1, row1, fin1);
     }
 }
 
