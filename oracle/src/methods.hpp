@@ -380,8 +380,10 @@ struct calculator {
                     if (z1_guess < tol) z1_guess = z1 * 0.5;
                     z1 = corr_lwc(z1, alpha_prev, sdc_scale_prev > 0.0 ? sdc_scale_prev : sdc_scale, z1_guess, alpha, sdc_scale);
                     lwc = z1 * p.max_water;
+#ifndef ORACLE_SKIP_DEAD_CSS  // the HIP kernel omits this call: its outputs are dead (tests/test_oracle_variants.py)
                     calc_snow_state(alpha, sdc_scale, p.initial_bare_ground_fraction, acc_melt, lwc, p.max_water, temp_swe,
                                     storage, sca);
+#endif
                 }
             }
             lwc += rain;

@@ -32,7 +32,7 @@ def load(variant: str = "detmath"):
     if variant in _CACHE:
         return _CACHE[variant]
     names = {"detmath": None, "libm": "liboracle_libm.so", "fullgamma": "liboracle_fullgamma.so",
-             "libm_fullgamma": "liboracle_libm_fullgamma.so"}
+             "libm_fullgamma": "liboracle_libm_fullgamma.so", "nodeadcss": "liboracle_nodeadcss.so"}
     path = LIB if variant == "detmath" else os.path.join(ORACLE_DIR, "_build", names[variant])
     if not os.path.exists(path):
         build()

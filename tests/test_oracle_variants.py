@@ -29,3 +29,20 @@ def test_detmath_vs_libm_oracle_c1():
     assert np.max(rel) < 1e-2
     # final Kirchner storage per cell
     assert np.max(np.abs(a["state"][:, 8] - b["state"][:, 8]) / b["state"][:, 8]) < 1e-5
+
+
+def test_post_brent_calc_snow_state_is_dead():
+    """gamma_snow's calc_snow_state right after corr_lwc (gamma_snow.h:433-434) only writes storage and sca, and
+    the step overwrites both before any read (the reset, or the final calc_snow_state, gamma_snow.h:472); the HIP
+    kernel therefore omits it (device/ptgsk_dev.h gs_back). The oracle built without it must give the same bits
+    as the reference-shaped oracle: config[0]'s region over the full year (every Brent job of a winter and an
+    autumn), all 8 response series and the final state."""
+    n, T = 200, 8760
+    geo = synthetic.geo11(n)
+    f = synthetic.forcing(n, 0, T)
+    p = synthetic.default_ptgsk_parameters()
+    s = synthetic.default_ptgsk_state(n)
+    a = oracle_lib.ptgsk_run(geo, p, s, synthetic.T0_2015_US, synthetic.HOUR_US, f, full=True, variant="detmath")
+    b = oracle_lib.ptgsk_run(geo, p, s, synthetic.T0_2015_US, synthetic.HOUR_US, f, full=True, variant="nodeadcss")
+    assert np.array_equal(a["full"], b["full"], equal_nan=True)
+    assert np.array_equal(a["state"], b["state"])
