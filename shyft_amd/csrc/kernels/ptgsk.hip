@@ -88,9 +88,11 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     gcell.inv_cv2 = cc[PC_INV_CV2 * N + lc];
     // the cell constants live in LDS, not in VGPRs: each use reloads its lane's slot (the barriers of the
     // step keep the compiler from hoisting the loads), so none of them is live across the Brent phase
-    // rows 0-9: the cell constants; rows 10-11: the lane's lgamma cache (shape, value), so that every per-lane LDS
-    // slot is one address register plus an immediate offset
-    __shared__ double lcc[12][B];
+    // rows 0-8: the cell constants; rows 9-10: the lane's lgamma cache (shape, value), so that every per-lane LDS
+    // slot is one address register plus an immediate offset. Two constants are formed from the others with the
+    // host's own expressions (region.hip update_derived): kirchner_fraction = 1 - direct_response_fraction and
+    // glacier_area_m2 = area * glacier, the same operations on the same doubles
+    __shared__ double lcc[11][B];
     {
         const int t = threadIdx.x;
         lcc[0][t] = gcell.forest_fraction;
@@ -101,16 +103,15 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         lcc[5][t] = cc[PC_SNOW_STORAGE * N + lc];
         lcc[6][t] = cc[PC_KIRCHNER_ROUTED_PREC * N + lc];
         lcc[7][t] = cc[PC_DIRECT_RESPONSE * N + lc];
-        lcc[8][t] = cc[PC_KIRCHNER_FRACTION * N + lc];
-        lcc[9][t] = cc[PC_AREA * N + lc];
+        lcc[8][t] = cc[PC_AREA * N + lc];
     }
 #define glacier_fraction (lcc[4][threadIdx.x])
 #define snow_storage_fraction (lcc[5][threadIdx.x])
 #define kirchner_routed_prec (lcc[6][threadIdx.x])
 #define direct_response_fraction (lcc[7][threadIdx.x])
-#define kirchner_fraction (lcc[8][threadIdx.x])
-#define cell_area_m2 (lcc[9][threadIdx.x])
-#define glacier_area_m2 (lcc[9][threadIdx.x] * lcc[4][threadIdx.x])  // PC_GLACIER_AREA = area * glacier (region.hip)
+#define kirchner_fraction (1 - lcc[7][threadIdx.x])                   // PC_KIRCHNER_FRACTION = 1 - direct
+#define cell_area_m2 (lcc[8][threadIdx.x])
+#define glacier_area_m2 (lcc[8][threadIdx.x] * lcc[4][threadIdx.x])  // PC_GLACIER_AREA = area * glacier
 #define LOAD_GCELL()                                   \
     do {                                               \
         gcell.forest_fraction = lcc[0][threadIdx.x];   \
@@ -133,9 +134,9 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     s.iso_pot_energy = st[PS_ISO_POT_ENERGY * N + lc];
     s.temp_swe = st[PS_TEMP_SWE * N + lc];
     double q = st[PS_KIRCHNER_Q * N + lc];
-    lcc[10][threadIdx.x] = -1.0;  // the lgamma cache (device/ptgsk_dev.h)
-    lcc[11][threadIdx.x] = 0.0;
-    lgamma_cache_lds lgc{lcc[10], lcc[11]};
+    lcc[9][threadIdx.x] = -1.0;  // the lgamma cache (device/ptgsk_dev.h)
+    lcc[10][threadIdx.x] = 0.0;
+    lgamma_cache_lds lgc{lcc[9], lcc[10]};
     gs_carry carry;
     int32_t err = 0;
 
@@ -154,9 +155,9 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
 
     // Brent job queue of the workgroup (COMPACT)
-    // (jres aliases jz1: a solving lane reads its job's z1 before it writes the job's result into the same slot)
-    __shared__ double jz1[B], ja1[B], jb1[B], ja2[B], jb2[B], jq1[B], jlg2[B];
-    double* const jres = jz1;
+    // (jres is not aliased with a job array: a lane reads its result after the step's second barrier, and another
+    // wavefront may already be enqueueing the next step's jobs by then)
+    __shared__ double jz1[B], ja1[B], jb1[B], ja2[B], jb2[B], jq1[B], jlg2[B], jres[B];
     __shared__ double jsz[SPEC ? 64 : 1], jsf[SPEC ? 64 : 1];  // speculative opening: point and f of lane t
     __shared__ int jcount[2];
     if (COMPACT) {
