@@ -60,11 +60,12 @@ STACKS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--launch", choices=("engine", "ranks"), default="engine",
-                    help="--gpus N > 1 without an outside launcher: 'engine' = this one process drives the N GPUs "
-                         "through a sharded region (shyft_hip_region_create_sharded: one shard per GPU, catchment / "
-                         "routing sums all-gathered by RCCL inside the engine); 'ranks' = start N rank processes "
-                         "(one per GPU, torch.distributed), as torch.distributed.run does")
+    ap.add_argument("--launch", choices=("engine", "ranks"), default=None,
+                    help="--gpus N > 1 without an outside launcher: 'ranks' (the default) = start N rank processes "
+                         "(one per GPU, torch.distributed), as torch.distributed.run does; 'engine' = this one process "
+                         "drives the N GPUs through a sharded region (shyft_hip_region_create_sharded: one shard per "
+                         "GPU, catchment / routing sums all-gathered by RCCL inside the engine after its self-check, "
+                         "device copies if RCCL fails). --gpus 1 --shards S always runs the engine's shards")
     ap.add_argument("--shards", type=int, default=0,
                     help="engine path: shards of the region (default: one per GPU); more shards than GPUs share "
                          "devices round-robin (on one GPU: --gpus 1 --shards 2 runs two shards on device 0)")
@@ -514,7 +515,7 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 
 
 def workload_tag(a, cells):
@@ -524,15 +525,21 @@ def workload_tag(a, cells):
 
 
 def pmc_summary(a, cells):
-    """The committed rocprofv3 PMC summary of the dominant kernel (profiles/r02/pmc_<workload>.json, written by
-    tools/gpu_profile.sh + tools/pmc_summary.py from this same bench command) or None. PMC counters cannot be
-    read from inside this process."""
-    path = os.path.join(PROFILE_DIR, f"pmc_{workload_tag(a, cells)}.json")
+    """(summary, reason): the committed rocprofv3 PMC summary of the dominant kernel
+    (profiles/<round>/pmc_<workload>.json, written by tools/gpu_profile.sh + tools/pmc_summary.py from this same
+    bench command) -- only if it measured THIS build of the library (same sha256), else (None, why). PMC counters
+    cannot be read from inside this process."""
+    from shyft_amd import _native
+    rel = f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json"
     try:
-        d = json.load(open(path))
+        d = json.load(open(os.path.join(ROOT, rel)))
     except (OSError, ValueError):
-        return None
-    return d
+        return None, f"no PMC summary of this workload ({rel})"
+    sha = _native.lib_sha()
+    if d.get("lib_sha256") != sha:
+        return None, (f"{rel} measured library sha256 {str(d.get('lib_sha256'))[:16]}, this run loads "
+                      f"{sha[:16]}: counters of another build are not reported")
+    return d, None
 
 
 def _cpu_model():
@@ -574,6 +581,8 @@ def dist_check(a, world, rank, pg):
 
 def main():
     a = parse()
+    if a.launch is None:
+        a.launch = "ranks" if a.gpus > 1 else "engine"
     engine = "WORLD_SIZE" not in os.environ and a.launch == "engine" and not a.dist_check
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not engine:
         sys.exit(launch_ranks(a.gpus))
@@ -636,7 +645,7 @@ def main():
     value = total_cell_steps / wall
     bytes_per_launch = cells * chunk * (read_b + write_b) + cells * state_b
     achieved = bytes_per_launch / (avg_kernel_ms * 1e-3)
-    pmc = pmc_summary(a, cells)
+    pmc, pmc_missing = pmc_summary(a, cells)
     traffic_b = None if pmc is None else pmc["traffic_bytes_per_launch"]
     out = {
         "metric": METRIC if a.stack == "pt_gs_k" else METRIC.replace("pt_gs_k", a.stack),
@@ -674,6 +683,7 @@ def main():
                             f"(shyft_hip_region_create_sharded), no data-path collective"
                             + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered inside "
                                f"the engine ({r.combine_path().upper()}) and added in shard order")
+                            + f"; combine: {r.combine_report()}"
                             if devices else
                             f"cells sharded over {world} GPU(s), one process each, no data-path collective"
                             + ("" if sums is None else "; per-chunk catchment discharge sums all-gathered "
@@ -691,8 +701,9 @@ def main():
             "frac": achieved / HBM_PEAK_BPS,
             "traffic": None if traffic_b is None else traffic_b / (avg_kernel_ms * 1e-3) / 1e9,
             "traffic_bytes_per_launch": traffic_b,
-            "traffic_source": (None if pmc is None else
-                               f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json: rocprofv3 "
+            "traffic_source": (pmc_missing if pmc is None else
+                               f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json "
+                               f"(library sha256 {pmc['lib_sha256'][:16]}, the one this run loaded): rocprofv3 "
                                f"FETCH_SIZE x {pmc['calibration']['fetch_correction']:.3f} + WRITE_SIZE x "
                                f"{pmc['calibration']['write_correction']:.3f} (gfx950 correction calibrated in the same "
                                "run, tools/pmc_summary.py), mean over the timed launches of this same command, over "

@@ -79,6 +79,22 @@ void shyft_hip_region_destroy(shyft_hip_region* h);
  * pointers: each shard's memory is on its own device). */
 int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* devices, size_t n_shards,
                                     shyft_hip_region** out);
+/* create_sharded with options. The combine path is chosen once, at creation: RCCL when every shard has its own
+ * device (or with SHYFT_HIP_SHARD_RCCL_ALWAYS: also one shard, a one-rank communicator), then a self-check before any
+ * data uses it -- an all-gather of known partials must arrive bit for bit on every device and their shard-order sum
+ * must equal the device-copy path's bitwise. A failed ncclCommInitAll, a failed self-check, or an RCCL error at run
+ * time switches the region to device copies (same results; shyft_hip_region_combine_report says why). No reference
+ * counterpart: the reference's one-process region has no exchange (core/region_model.h:972-1021).
+ * SHYFT_HIP_SHARD_NO_RCCL: device copies only. The TEST_ flags inject the failures for the fallback tests:
+ * ncclCommInitAll failing, the first all-gather after the self-check failing, the self-check comparing unequal. */
+enum shyft_hip_shard_flags {
+    SHYFT_HIP_SHARD_RCCL_ALWAYS = 1, SHYFT_HIP_SHARD_NO_RCCL = 2, SHYFT_HIP_SHARD_TEST_FAIL_INIT = 4,
+    SHYFT_HIP_SHARD_TEST_FAIL_GATHER = 8, SHYFT_HIP_SHARD_TEST_CORRUPT_CHECK = 16
+};
+int shyft_hip_region_create_sharded_ex(int stack, size_t n_cells, const int* devices, size_t n_shards, unsigned flags,
+                                       shyft_hip_region** out);
+/* One line: the combine path, why it was chosen, the self-check result and any run-time fallback ("" unsharded). */
+const char* shyft_hip_region_combine_report(const shyft_hip_region* h);
 /* Number of shards (1 for an unsharded region); for k below it, shard k's device, first cell and cell count. */
 size_t shyft_hip_region_shards(const shyft_hip_region* h, size_t k, int* device, size_t* cell0, size_t* n_cells);
 /* How the shards' partial sums are combined: SHYFT_HIP_COMBINE_NONE (unsharded), _COPY (device copies), _RCCL. */
@@ -204,9 +220,9 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
 int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next);
 /* Milliseconds of the last run_cells kernel launch(es), timed with HIP events on the region's stream. */
 double shyft_hip_last_run_ms(const shyft_hip_region* h);
-/* The last run's kernels separately: pt_gs_k runs as two kernels (gamma_snow, then glacier/PT/AE/kirchner), the
-   other stacks as one. Fills ms[0..min(n, parts)) and returns the number of parts. (No reference counterpart:
-   measurement only.) */
+/* The last run's kernels separately: every stack runs one kernel per run_cells, so parts is 1 (ms[0] = the kernel;
+   a sharded region: the slowest running shard's). Fills ms[0..min(n, parts)) and returns the number of parts.
+   (No reference counterpart: measurement only.) */
 int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n);
 
 /* Response series for steps [step0, step0+n), [n][n_cells]. */
@@ -243,6 +259,11 @@ int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out);
  * core/cell_model.h:47-81,112-160): steps [step0, step0+n) copied to/from buf[n].
  * write != 0 is allowed for forcing only (env_ts.<var>.set(i, v)). series uses the ids above. */
 int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t step0, size_t n, double* buf, int write);
+/* Many cells' views at once (the per-cell collector series of region_model::get_cells(), read in bulk): columns
+ * cells[n_cells] of series `series` (ids as above), steps [step0, step0+n) of the resident window, into host
+ * dst[n][n_cells]. One gather on the device (per shard for a sharded region). */
+int shyft_hip_sample_cells(const shyft_hip_region* h, int series, const int64_t* cells, size_t n_cells, size_t step0,
+                           size_t n, double* dst);
 
 /* region_model::is_cell_env_ts_ok (core/region_model.h:954-962): *ok = 1 when no forcing value of a
  * calculated cell (catchment filter) in the resident window is NaN. */

@@ -26,7 +26,10 @@ SIGNATURES = {
     "shyft_hip_region_destroy": (None, [_h]),
     "shyft_hip_region_create_sharded": (C.c_int, [C.c_int, C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "shyft_hip_region_shards": (C.c_size_t, [_h, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "shyft_hip_region_create_sharded_ex": (C.c_int, [C.c_int, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint,
+                                                     C.POINTER(C.c_void_p)]),
     "shyft_hip_region_combine_path": (C.c_int, [_h]),
+    "shyft_hip_region_combine_report": (C.c_char_p, [_h]),
     "shyft_hip_region_size": (C.c_size_t, [_h]),
     "shyft_hip_set_geo": (C.c_int, [_h, C.c_void_p, C.c_void_p, C.c_void_p]),
     "shyft_hip_set_parameters": (C.c_int, [_h, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]),
@@ -66,6 +69,7 @@ SIGNATURES = {
     "shyft_hip_catchment_ids": (C.c_int, [_h, C.c_void_p]),
     "shyft_hip_region_clone": (C.c_int, [_h, C.POINTER(C.c_void_p)]),
     "shyft_hip_cell_series": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
+    "shyft_hip_sample_cells": (C.c_int, [_h, C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p]),
     "shyft_hip_forcing_ok": (C.c_int, [_h, C.POINTER(C.c_int)]),
     "shyft_hip_set_routing_groups": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_routing_group_sums": (C.c_int, [_h, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
@@ -85,6 +89,17 @@ def header_symbols(header: str | None = None) -> list[str]:
     header = header or os.path.join(os.path.dirname(_HERE), "include", "shyft_hip.h")
     src = open(header).read()
     return sorted(set(re.findall(r"\b(shyft_hip_[a-z_0-9]+)\s*\(", src)))
+
+
+def lib_sha(path: str | None = None) -> str:
+    """sha256 of the C ABI library file (the build identity the committed PMC summaries are keyed on:
+    a summary measured on another build of the kernels is not this build's traffic)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path or LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
 
 
 def _preload_hip_runtime() -> None:

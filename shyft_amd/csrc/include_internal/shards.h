@@ -7,7 +7,8 @@
 
 namespace shyft_hip_impl {
 
-shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_t n_shards);  // throws
+shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_t n_shards,
+                            unsigned flags);  // throws
 void shard_set_destroy(shard_set* s);
 
 // region.hip: sum over the selected cells of one region (select_cells semantics), value x cell area when weighted;
@@ -18,6 +19,8 @@ int region_selected_sums(shyft_hip_region* h, int series, const int64_t* ids, si
 namespace shards {
 size_t info(const shard_set* s, size_t k, int* device, size_t* cell0, size_t* n_cells);
 int combine_path(const shard_set* s);
+const char* combine_report(const shard_set* s);
+void sample_cells(shard_set* s, int series, const int64_t* cells, size_t n_cells, size_t step0, size_t n, double* dst);
 void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double* rdist);
 void set_parameters(shard_set* s, const double* params, size_t n_sets, size_t n_per_set, const int32_t* set_ix);
 void set_time_axis(shard_set* s, int64_t t0, int64_t dt, size_t n_steps, size_t window);

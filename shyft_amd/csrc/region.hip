@@ -377,6 +377,15 @@ int shyft_hip_region_create(int stack, size_t n_cells, int device, shyft_hip_reg
 
 int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* devices, size_t n_shards,
                                     shyft_hip_region** out) {
+    return shyft_hip_region_create_sharded_ex(stack, n_cells, devices, n_shards, 0u, out);
+}
+
+const char* shyft_hip_region_combine_report(const shyft_hip_region* h) {
+    return h && h->sh ? shards::combine_report(h->sh) : "";
+}
+
+int shyft_hip_region_create_sharded_ex(int stack, size_t n_cells, const int* devices, size_t n_shards, unsigned flags,
+                                       shyft_hip_region** out) {
     if (!out) return fail(nullptr, "shyft_hip_region_create_sharded: out is null");
     *out = nullptr;
     if (stack != SHYFT_HIP_PT_GS_K && stack != SHYFT_HIP_HBV_STACK && stack != SHYFT_HIP_PT_SS_K &&
@@ -388,7 +397,7 @@ int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* device
         h->stack = stack;
         h->n = n_cells;
         h->device = devices && n_shards ? devices[0] : 0;
-        h->sh = shard_set_create(stack, n_cells, devices, n_shards);
+        h->sh = shard_set_create(stack, n_cells, devices, n_shards, flags);
         *out = h.release();
         return 0;
     } catch (const std::exception& e) {
@@ -1435,6 +1444,27 @@ int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t s
             hip_check(hipMemcpy2DAsync(buf, sizeof(double), p, pitch, sizeof(double), n, hipMemcpyDeviceToHost, h->stream),
                       "cell_series read");
         hip_check(hipStreamSynchronize(h->stream), "sync");
+    });
+}
+
+int shyft_hip_sample_cells(const shyft_hip_region* hc, int series, const int64_t* cells, size_t n_cells, size_t step0,
+                           size_t n, double* dst) {
+    shyft_hip_region* h = const_cast<shyft_hip_region*>(hc);
+    if (!h || (n_cells && (!cells || !dst))) return fail(h, "shyft_hip_sample_cells: null argument");
+    if (n_cells == 0 || n == 0) return 0;
+    if (h->sh) return guarded(h, [&] { shards::sample_cells(h->sh, series, cells, n_cells, step0, n, dst); });
+    return guarded(h, [&] {
+        const double* rows = series_rows(h, series, step0, n, "sample_cells");
+        std::vector<int32_t> idx(n_cells);
+        for (size_t j = 0; j < n_cells; ++j) {
+            if (cells[j] < 0 || size_t(cells[j]) >= h->n) throw std::runtime_error("sample_cells: cell index out of range");
+            idx[j] = int32_t(cells[j]);
+        }
+        h->d_sel.alloc(std::max(h->d_sel.n, n_cells));
+        hip_check(region_copy(h, h->d_sel.p, idx.data(), n_cells * sizeof(int32_t), hipMemcpyHostToDevice), "upload cells");
+        h->d_tmp.alloc(std::max(h->d_tmp.n, n * n_cells));
+        hip_check(launch_gather_columns(h->d_tmp.p, rows, n, h->n, h->d_sel.p, n_cells, h->stream), "gather_columns");
+        copy_rows(h->stream, dst, h->d_tmp.p, n * n_cells * sizeof(double), 0, 1);
     });
 }
 

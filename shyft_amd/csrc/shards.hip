@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <exception>
 #include <map>
 #include <memory>
@@ -50,6 +51,9 @@ struct shard_set {
     std::vector<hipStream_t> streams;  // one per shard, on its device
     std::vector<std::unique_ptr<shard_bufs>> bufs;
     int path = SHYFT_HIP_COMBINE_COPY;
+    unsigned flags = 0;                // SHYFT_HIP_SHARD_* options of shyft_hip_region_create_sharded_ex
+    std::string report;                // how the combine path was chosen, its self-check, run-time fallbacks
+    bool gather_fail_armed = false;    // SHYFT_HIP_SHARD_TEST_FAIL_GATHER: the next all-gather fails
     size_t ens_members = 0;
 
     size_t S() const { return r.size(); }
@@ -102,6 +106,157 @@ void join_cols(const std::vector<double>& src, size_t N, size_t n, size_t b, siz
     for (size_t t = 0; t < n; ++t) std::copy(src.begin() + t * nk, src.begin() + (t + 1) * nk, dst + t * N + b);
 }
 
+void drop_comms(shard_set* s) {
+    for (auto& c : s->comms)
+        if (c) (void)ncclCommAbort(c);
+    s->comms.clear();
+}
+
+// the all-gather step of combine(): bufs[k]->full [M] of every shard -> [S][M] partials on shard 0's device in
+// bufs[0]->gath (RCCL: on every shard's device). An RCCL failure at run time (an error status from the group) drops
+// the communicators and switches the region to device copies for this and every later combine: the reference's
+// one-process region has no exchange that can fail, so a failing interconnect costs speed, never a result.
+void exchange(shard_set* s, size_t M) {
+    const size_t S = s->S();
+    if (s->path == SHYFT_HIP_COMBINE_RCCL) {
+        try {
+            if (s->gather_fail_armed) {
+                s->gather_fail_armed = false;
+                throw std::runtime_error("ncclAllGather: injected failure (SHYFT_HIP_SHARD_TEST_FAIL_GATHER)");
+            }
+            nccl_check(ncclGroupStart(), "ncclGroupStart");
+            for (size_t k = 0; k < S; ++k) {
+                hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+                nccl_check(ncclAllGather(s->bufs[k]->full.p, s->bufs[k]->gath.p, M, ncclDouble, s->comms[k], s->streams[k]),
+                           "ncclAllGather");
+            }
+            nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+            for (size_t k = 0; k < S; ++k) {
+                hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+                hip_check(hipStreamSynchronize(s->streams[k]), "ncclAllGather completion");
+            }
+            hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
+            return;
+        } catch (const std::exception& e) {
+            for (size_t k = 0; k < S; ++k) {
+                (void)hipSetDevice(s->dev[k]);
+                (void)hipStreamSynchronize(s->streams[k]);
+            }
+            drop_comms(s);
+            s->path = SHYFT_HIP_COMBINE_COPY;
+            s->report += std::string("; RCCL failed at run time (") + e.what() + "): device copies from then on";
+        }
+    }
+    hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
+    for (size_t k = 0; k < S; ++k)
+        hip_check(hipMemcpyPeerAsync(s->bufs[0]->gath.p + k * M, s->dev[0], s->bufs[k]->full.p, s->dev[k],
+                                     M * sizeof(double), s->streams[0]),
+                  "gather partials");
+}
+
+// The first RCCL use of a region, before any data goes through it: every shard contributes M known doubles
+// (signed, spread over 60 binades), the all-gather must deliver all S x M bit for bit on every device, and the
+// shard-order sum of the gathered partials must equal the one of the device-copy path bitwise. Any mismatch or
+// error is returned as text (empty: passed).
+std::string rccl_self_check(shard_set* s) {
+    const size_t S = s->S(), M = 4096;
+    std::vector<std::vector<double>> in(S, std::vector<double>(M));
+    for (size_t k = 0; k < S; ++k)
+        for (size_t j = 0; j < M; ++j) {
+            const double m = double((k * 2654435761ull + j * 40503ull) % 1000003ull) + 0.5;
+            in[k][j] = std::ldexp((j & 1) ? -m : m, int(j % 61) - 30);
+        }
+    try {
+        for (size_t k = 0; k < S; ++k) {
+            hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+            shard_bufs& q = *s->bufs[k];
+            q.full.alloc(M);
+            q.gath.alloc(S * M);
+            q.out.alloc(M);
+            hip_check(hipMemcpyAsync(q.full.p, in[k].data(), M * sizeof(double), hipMemcpyHostToDevice, s->streams[k]),
+                      "self-check upload");
+            hip_check(hipStreamSynchronize(s->streams[k]), "self-check upload");
+        }
+        exchange(s, M);
+        if (s->path != SHYFT_HIP_COMBINE_RCCL) return "the all-gather failed";
+        std::vector<double> got(S * M);
+        for (size_t k = 0; k < S; ++k) {
+            hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+            hip_check(hipMemcpy(got.data(), s->bufs[k]->gath.p, S * M * sizeof(double), hipMemcpyDeviceToHost),
+                      "self-check download");
+            for (size_t r = 0; r < S; ++r)
+                if (std::memcmp(got.data() + r * M, in[r].data(), M * sizeof(double)) != 0)
+                    return "device " + std::to_string(s->dev[k]) + " received shard " + std::to_string(r) +
+                           "'s partials with different bits";
+        }
+        hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
+        shard_bufs& q0 = *s->bufs[0];
+        std::vector<double> sum_rccl(M), sum_copy(M);
+        hip_check(launch_ordered_sum(q0.gath.p, S, M, q0.out.p, s->streams[0]), "ordered_sum");
+        hip_check(hipMemcpyAsync(sum_rccl.data(), q0.out.p, M * sizeof(double), hipMemcpyDeviceToHost, s->streams[0]),
+                  "self-check download");
+        hip_check(hipMemsetAsync(q0.gath.p, 0xff, S * M * sizeof(double), s->streams[0]), "memset");
+        for (size_t k = 0; k < S; ++k)
+            hip_check(hipMemcpyPeerAsync(q0.gath.p + k * M, s->dev[0], s->bufs[k]->full.p, s->dev[k], M * sizeof(double),
+                                         s->streams[0]),
+                      "self-check copy path");
+        hip_check(launch_ordered_sum(q0.gath.p, S, M, q0.out.p, s->streams[0]), "ordered_sum");
+        hip_check(hipMemcpyAsync(sum_copy.data(), q0.out.p, M * sizeof(double), hipMemcpyDeviceToHost, s->streams[0]),
+                  "self-check download");
+        hip_check(hipStreamSynchronize(s->streams[0]), "self-check");
+        if (s->flags & SHYFT_HIP_SHARD_TEST_CORRUPT_CHECK) sum_rccl[M / 2] = std::nextafter(sum_rccl[M / 2], 0.0);
+        if (std::memcmp(sum_rccl.data(), sum_copy.data(), M * sizeof(double)) != 0)
+            return "shard-order sums of the RCCL and the device-copy gathers differ";
+        return "";
+    } catch (const std::exception& e) {
+        return e.what();
+    }
+}
+
+// the combine path of a new region (shard_set_create, clone): RCCL when every shard has its own device (or when
+// asked for), verified by rccl_self_check; otherwise, or on any RCCL failure, device copies
+void choose_path(shard_set* s) {
+    const size_t S = s->S();
+    std::vector<int> sorted(s->dev);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    std::string devs;
+    for (size_t k = 0; k < S; ++k) devs += (k ? "," : "") + std::to_string(s->dev[k]);
+    s->path = SHYFT_HIP_COMBINE_COPY;
+    if (s->flags & SHYFT_HIP_SHARD_NO_RCCL) {
+        s->report = "copy: RCCL not requested (SHYFT_HIP_SHARD_NO_RCCL)";
+        return;
+    }
+    const bool want = (S > 1 && distinct) || (s->flags & SHYFT_HIP_SHARD_RCCL_ALWAYS);
+    if (!want) {
+        // RCCL does not put two ranks of one communicator on one device
+        s->report = S > 1 ? "copy: shards share a device (devices " + devs + ")" : "copy: one shard";
+        return;
+    }
+    try {
+        if (s->flags & SHYFT_HIP_SHARD_TEST_FAIL_INIT)
+            throw std::runtime_error("ncclCommInitAll: injected failure (SHYFT_HIP_SHARD_TEST_FAIL_INIT)");
+        s->comms.assign(S, nullptr);
+        nccl_check(ncclCommInitAll(s->comms.data(), int(S), s->dev.data()), "ncclCommInitAll");
+    } catch (const std::exception& e) {
+        drop_comms(s);
+        s->report = std::string("copy: RCCL initialisation failed (") + e.what() + "), device copies instead";
+        return;
+    }
+    s->path = SHYFT_HIP_COMBINE_RCCL;
+    const std::string bad = rccl_self_check(s);
+    if (!bad.empty()) {
+        drop_comms(s);
+        s->path = SHYFT_HIP_COMBINE_COPY;
+        s->report = "copy: RCCL self-check failed (" + bad + "), device copies instead";
+        return;
+    }
+    s->report = "rccl: ncclCommInitAll over devices " + devs + "; self-check passed (all-gather of " +
+                std::to_string(S) + " x 4096 known doubles bit-exact on every device, shard-order sums bit-equal to "
+                "the device-copy path)";
+    s->gather_fail_armed = (s->flags & SHYFT_HIP_SHARD_TEST_FAIL_GATHER) != 0;
+}
+
 // The combination of per-shard partial sums (see the file header). part(k, dev_ptr) writes shard k's partial
 // [R_k][n] to a device buffer on its device and returns R_k; rowmap(k) maps its rows to the R global rows (empty:
 // identity, R_k == R). The result [R][n] is written to dst (host, or a device pointer on shard 0's device).
@@ -134,23 +289,8 @@ void combine(shard_set* s, size_t R, size_t n, Part&& part, RowMap&& rowmap, dou
         }
         hip_check(hipStreamSynchronize(s->streams[k]), "partials");
     });
-    if (s->path == SHYFT_HIP_COMBINE_RCCL) {
-        nccl_check(ncclGroupStart(), "ncclGroupStart");
-        for (size_t k = 0; k < S; ++k) {
-            hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
-            nccl_check(ncclAllGather(s->bufs[k]->full.p, s->bufs[k]->gath.p, M, ncclDouble, s->comms[k], s->streams[k]),
-                       "ncclAllGather");
-        }
-        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-        // every device holds the same gathered partials; shard 0's device sums them for the caller
-        hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
-    } else {
-        hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
-        for (size_t k = 0; k < S; ++k)
-            hip_check(hipMemcpyPeerAsync(s->bufs[0]->gath.p + k * M, s->dev[0], s->bufs[k]->full.p, s->dev[k],
-                                         M * sizeof(double), s->streams[0]),
-                      "gather partials");
-    }
+    // RCCL: every device holds the same gathered partials; shard 0's device sums them for the caller
+    exchange(s, M);
     shard_bufs& q0 = *s->bufs[0];
     double* out = dst_on_device ? dst : q0.out.p;
     hip_check(launch_ordered_sum(q0.gath.p, S, M, out, s->streams[0]), "ordered_sum");
@@ -185,7 +325,7 @@ std::vector<int32_t> catchment_rows(const shard_set* s, size_t k) {
 
 }  // namespace
 
-shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_t n_shards) {
+shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_t n_shards, unsigned flags) {
     if (n_shards == 0 || !devices) throw std::runtime_error("shyft_hip_region_create_sharded: no devices");
     if (n_cells < n_shards) throw std::runtime_error("shyft_hip_region_create_sharded: fewer cells than shards");
     int n_dev = 0;
@@ -197,43 +337,38 @@ shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_
     std::unique_ptr<shard_set, void (*)(shard_set*)> s(new shard_set(), shard_set_destroy);
     s->stack = stack;
     s->n = n_cells;
+    s->flags = flags;
+    // every per-shard vector is complete before any shard resource exists, so a failure part-way (a shard that
+    // cannot be allocated) unwinds through shard_set_destroy with consistent indexes
     for (size_t k = 0; k < n_shards; ++k) {
-        const size_t b = n_cells * k / n_shards, e = n_cells * (k + 1) / n_shards;
-        shyft_hip_region* c = nullptr;
-        if (shyft_hip_region_create(stack, e - b, devices[k], &c)) throw std::runtime_error(shyft_hip_last_error(nullptr));
-        s->r.push_back(c);
-        s->b.push_back(b);
-        s->e.push_back(e);
+        s->b.push_back(n_cells * k / n_shards);
+        s->e.push_back(n_cells * (k + 1) / n_shards);
         s->dev.push_back(devices[k]);
         s->idle.push_back(0);
+    }
+    for (size_t k = 0; k < n_shards; ++k) {
+        shyft_hip_region* c = nullptr;
+        if (shyft_hip_region_create(stack, s->e[k] - s->b[k], devices[k], &c))
+            throw std::runtime_error(shyft_hip_last_error(nullptr));
+        s->r.push_back(c);
         hipStream_t st = nullptr;
         hip_check(hipSetDevice(devices[k]), "hipSetDevice");
         hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
         s->streams.push_back(st);
         s->bufs.emplace_back(new shard_bufs());
     }
-    std::vector<int> sorted(s->dev);
-    std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (n_shards > 1 && distinct) {
-        s->comms.resize(n_shards);
-        nccl_check(ncclCommInitAll(s->comms.data(), int(n_shards), s->dev.data()), "ncclCommInitAll");
-        s->path = SHYFT_HIP_COMBINE_RCCL;
-    } else {
-        // shards sharing a device (or one shard): the partials are copied device to device (hipMemcpyPeerAsync),
-        // RCCL does not put two ranks of one communicator on one device
-        s->path = SHYFT_HIP_COMBINE_COPY;
-    }
+    choose_path(s.get());
     return s.release();
 }
 
 void shard_set_destroy(shard_set* s) {
     if (!s) return;
-    for (auto& c : s->comms) (void)ncclCommDestroy(c);
+    for (auto& c : s->comms)
+        if (c) (void)ncclCommDestroy(c);
     for (size_t k = 0; k < s->streams.size(); ++k) {
         (void)hipSetDevice(s->dev[k]);
         (void)hipStreamSynchronize(s->streams[k]);
-        s->bufs[k].reset();  // device buffers freed on their device
+        if (k < s->bufs.size()) s->bufs[k].reset();  // device buffers freed on their device
         (void)hipStreamDestroy(s->streams[k]);
     }
     for (auto* c : s->r) shyft_hip_region_destroy(c);
@@ -252,6 +387,8 @@ size_t info(const shard_set* s, size_t k, int* device, size_t* cell0, size_t* n_
 }
 
 int combine_path(const shard_set* s) { return s->path; }
+
+const char* combine_report(const shard_set* s) { return s->report.c_str(); }
 
 void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double* rdist) {
     for_shards(s, [&](size_t k) {
@@ -291,9 +428,12 @@ void set_catchment_filter(shard_set* s, const int64_t* cids, size_t n) {
                 throw std::runtime_error("set_catchment_calculation_filter: no cells have supplied cid");
     }
     for_shards(s, [&](size_t k) {
+        // each catchment once: a list with repeats that passed the region's check must not fail a shard's
+        // "supplied list > available catchments" check because that shard holds fewer catchments
         std::vector<int64_t> mine;
         for (size_t j = 0; j < n; ++j)
-            if (std::find(s->child_cids[k].begin(), s->child_cids[k].end(), cids[j]) != s->child_cids[k].end())
+            if (std::find(s->child_cids[k].begin(), s->child_cids[k].end(), cids[j]) != s->child_cids[k].end() &&
+                std::find(mine.begin(), mine.end(), cids[j]) == mine.end())
                 mine.push_back(cids[j]);
         s->idle[k] = n > 0 && mine.empty();
         ck(s->r[k], shyft_hip_set_catchment_filter(s->r[k], mine.empty() ? nullptr : mine.data(), mine.size()));
@@ -411,6 +551,7 @@ int last_run_kernel_ms(const shard_set* s, double* ms, int n) {
     int parts = 1;
     std::vector<double> mx(4, 0.0);
     for (size_t k = 0; k < s->S(); ++k) {
+        if (s->idle[k]) continue;  // not run: its timing is from an earlier run (as last_run_ms)
         double v[4] = {0, 0, 0, 0};
         parts = shyft_hip_last_run_kernel_ms(s->r[k], v, 4);
         for (int j = 0; j < 4; ++j) mx[size_t(j)] = std::max(mx[size_t(j)], v[j]);
@@ -424,6 +565,26 @@ void cell_series(shard_set* s, int series, size_t cell, size_t step0, size_t n, 
     const size_t k = s->shard_of(cell);
     hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
     ck(s->r[k], shyft_hip_cell_series(s->r[k], series, cell - s->b[k], step0, n, buf, write));
+}
+
+// columns of selected cells: each shard gathers the ones it holds, into their columns of dst [n][n_cells]
+void sample_cells(shard_set* s, int series, const int64_t* cells, size_t m, size_t step0, size_t n, double* dst) {
+    std::vector<std::vector<int64_t>> loc(s->S());
+    std::vector<std::vector<size_t>> col(s->S());
+    for (size_t j = 0; j < m; ++j) {
+        if (cells[j] < 0 || size_t(cells[j]) >= s->n) throw std::runtime_error("sample_cells: cell index out of range");
+        const size_t k = s->shard_of(size_t(cells[j]));
+        loc[k].push_back(cells[j] - int64_t(s->b[k]));
+        col[k].push_back(j);
+    }
+    for_shards(s, [&](size_t k) {
+        const size_t mk = loc[k].size();
+        if (mk == 0) return;
+        std::vector<double> blk(n * mk);
+        ck(s->r[k], shyft_hip_sample_cells(s->r[k], series, loc[k].data(), mk, step0, n, blk.data()));
+        for (size_t t = 0; t < n; ++t)
+            for (size_t q = 0; q < mk; ++q) dst[t * m + col[k][q]] = blk[t * mk + q];
+    });
 }
 
 void forcing_ok(shard_set* s, int* ok) {
@@ -566,6 +727,16 @@ shard_set* clone(const shard_set* src) {
     std::unique_ptr<shard_set, void (*)(shard_set*)> s(new shard_set(), shard_set_destroy);
     s->stack = src->stack;
     s->n = src->n;
+    // host members first (shard_set_destroy reads dev[k] for every stream created below, on any failure)
+    s->b = src->b;
+    s->e = src->e;
+    s->dev = src->dev;
+    s->idle = src->idle;
+    s->cix_to_cid = src->cix_to_cid;
+    s->cid_to_cix = src->cid_to_cix;
+    s->child_cids = src->child_cids;
+    s->n_groups = src->n_groups;
+    s->flags = src->flags & ~unsigned(SHYFT_HIP_SHARD_TEST_FAIL_GATHER);
     for (size_t k = 0; k < src->S(); ++k) {
         hip_check(hipSetDevice(src->dev[k]), "hipSetDevice");
         shyft_hip_region* c = nullptr;
@@ -576,19 +747,14 @@ shard_set* clone(const shard_set* src) {
         s->streams.push_back(st);
         s->bufs.emplace_back(new shard_bufs());
     }
-    s->b = src->b;
-    s->e = src->e;
-    s->dev = src->dev;
-    s->idle = src->idle;
-    s->cix_to_cid = src->cix_to_cid;
-    s->cid_to_cix = src->cid_to_cix;
-    s->child_cids = src->child_cids;
-    s->n_groups = src->n_groups;
+    // the clone's own communicators (and self-check) if the source combines by RCCL; a source that fell back to
+    // copies stays on copies
     if (src->path == SHYFT_HIP_COMBINE_RCCL) {
-        s->comms.resize(s->S());
-        nccl_check(ncclCommInitAll(s->comms.data(), int(s->S()), s->dev.data()), "ncclCommInitAll");
+        choose_path(s.get());
+    } else {
+        s->path = src->path;
+        s->report = src->report;
     }
-    s->path = src->path;
     return s.release();
 }
 

@@ -26,6 +26,9 @@ HBV_MAX_BINS = 8
 HBV_STATE = (("swe", "sca", "soil_moisture", "tank_uz", "tank_lz", "n_bins") +
              tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) + tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
 SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
+SERIES_FORCING, SERIES_STATE = 100, 200
+# shyft_hip_region_create_sharded_ex options (include/shyft_hip.h)
+SHARD_RCCL_ALWAYS, SHARD_NO_RCCL, SHARD_TEST_FAIL_INIT, SHARD_TEST_FAIL_GATHER, SHARD_TEST_CORRUPT_CHECK = 1, 2, 4, 8, 16
 # pt_ss_k (core/pt_ss_k.h:154-181, pt_ss_k_cell_model.h:38-200); response series ids are the pt_gs_k ones
 PTSSK_STATE = ("nu", "alpha", "sca", "swe", "free_water", "residual", "num_units", "kirchner_q")
 PTSSK_STATE_SERIES = ("kirchner_discharge", "snow_sca", "snow_swe", "snow_alpha", "snow_nu", "snow_lwc",
@@ -58,14 +61,15 @@ class HipRegion:
     whose cells are split into len(devices) contiguous shards driven from this process
     (shyft_hip_region_create_sharded): every method below then works on the whole region."""
 
-    def __init__(self, stack: int, n_cells: int, device: int = -1, devices=None):
+    def __init__(self, stack: int, n_cells: int, device: int = -1, devices=None, shard_flags: int = 0):
         self._L = lib()
         h = C.c_void_p()
         if devices is None:
             check(self._L.shyft_hip_region_create(stack, n_cells, device, C.byref(h)), None)
         else:
             d = np.ascontiguousarray(list(devices), dtype=np.int32)
-            check(self._L.shyft_hip_region_create_sharded(stack, n_cells, _ptr(d), d.size, C.byref(h)), None)
+            check(self._L.shyft_hip_region_create_sharded_ex(stack, n_cells, _ptr(d), d.size, int(shard_flags),
+                                                             C.byref(h)), None)
         self.h = h
         self.stack = stack
         self.n = n_cells
@@ -85,6 +89,11 @@ class HipRegion:
     def combine_path(self) -> str:
         """How shard partial sums are combined: "none" (unsharded), "copy" (shards share a device), "rccl"."""
         return ("none", "copy", "rccl")[int(self._L.shyft_hip_region_combine_path(self.h))]
+
+    def combine_report(self) -> str:
+        """The combine path's decision: why RCCL or copies, the RCCL self-check result, run-time fallbacks."""
+        r = self._L.shyft_hip_region_combine_report(self.h)
+        return r.decode() if r else ""
 
     def close(self):
         if getattr(self, "h", None):
@@ -231,6 +240,14 @@ class HipRegion:
     def get_state_series(self, field: int, step0: int, n: int) -> np.ndarray:
         out = np.empty((n, self.n), dtype=np.float64)
         self._chk(self._L.shyft_hip_get_state_series(self.h, field, step0, n, _ptr(out), 0))
+        return out
+
+    def sample_cells(self, series: int, cells, step0: int, n: int) -> np.ndarray:
+        """[n][len(cells)] columns of a series (response id, SERIES_FORCING + v, SERIES_STATE + f) for the given
+        cells over steps [step0, step0 + n) of the resident window (one device gather; per shard if sharded)."""
+        c = np.ascontiguousarray(cells, dtype=np.int64)
+        out = np.empty((n, c.size), dtype=np.float64)
+        self._chk(self._L.shyft_hip_sample_cells(self.h, int(series), _ptr(c), c.size, int(step0), int(n), _ptr(out)))
         return out
 
     def statistics(self, series: int, ids=(), scope: int = SCOPE_CATCHMENT, weighted: bool = False, step0: int = 0,

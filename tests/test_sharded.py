@@ -197,3 +197,150 @@ def test_api_model_with_devices():
     c = pt_gs_k.create_opt_model_clone(b)
     assert list(c.shard_devices) == [0, 0]
     c.run_cells()
+
+
+# ---- the combine path's choice, self-check and fallbacks (shyft_hip_region_create_sharded_ex) ----
+# On a one-GPU box RCCL_ALWAYS makes a one-shard region build a one-rank communicator, so ncclCommInitAll, the
+# self-check's ncclAllGather and the run-time all-gathers execute on the hardware; the TEST_ flags inject the failures
+# whose fallback must leave every result unchanged.
+
+def _sums_vs_unsharded(sh, stack="pt_gs_k"):
+    ref = _region(stack, None)
+    try:
+        _run(ref)
+        _run(sh)
+        assert _same(sh.catchment_sums(0, 0, T), ref.catchment_sums(0, 0, T))
+        assert _same(sh.get_series(0, 0, T), ref.get_series(0, 0, T))
+    finally:
+        ref.close()
+
+
+def _flagged(flags, devices=(0,)):
+    from shyft_amd.region import HipRegion, COLLECT_ALL
+    import bench
+    r = HipRegion(1, N, devices=list(devices), shard_flags=flags)
+    r.set_geo(synthetic.geo11(N, n_catchments=C))
+    r.set_parameters(bench.stack_defaults("pt_gs_k", 1)[0])
+    r.set_time_axis(synthetic.T0_2015_US, HOUR, T)
+    r.set_collection(COLLECT_ALL)
+    r.set_state(bench.stack_defaults("pt_gs_k", N)[1])
+    return r
+
+
+def test_rccl_one_rank_self_check_and_sums():
+    from shyft_amd.region import SHARD_RCCL_ALWAYS
+    sh = _flagged(SHARD_RCCL_ALWAYS)
+    try:
+        assert sh.combine_path() == "rccl", sh.combine_report()
+        assert "self-check passed" in sh.combine_report()
+        _sums_vs_unsharded(sh)
+        assert sh.combine_path() == "rccl", sh.combine_report()     # no run-time fallback happened
+        c = sh.__class__.__new__(sh.__class__)                       # a clone builds and checks its own communicator
+        import ctypes as C
+        h = C.c_void_p()
+        assert sh._L.shyft_hip_region_clone(sh.h, C.byref(h)) == 0
+        c._L, c.h, c.stack, c.n = sh._L, h, sh.stack, sh.n
+        try:
+            assert c.combine_path() == "rccl" and "self-check passed" in c.combine_report()
+        finally:
+            c.close()
+    finally:
+        sh.close()
+
+
+def test_rccl_init_failure_falls_back_to_copies():
+    from shyft_amd.region import SHARD_RCCL_ALWAYS, SHARD_TEST_FAIL_INIT
+    sh = _flagged(SHARD_RCCL_ALWAYS | SHARD_TEST_FAIL_INIT)
+    try:
+        assert sh.combine_path() == "copy"
+        assert "initialisation failed" in sh.combine_report() and "injected" in sh.combine_report()
+        _sums_vs_unsharded(sh)
+    finally:
+        sh.close()
+
+
+def test_rccl_self_check_mismatch_falls_back_to_copies():
+    from shyft_amd.region import SHARD_RCCL_ALWAYS, SHARD_TEST_CORRUPT_CHECK
+    sh = _flagged(SHARD_RCCL_ALWAYS | SHARD_TEST_CORRUPT_CHECK)
+    try:
+        assert sh.combine_path() == "copy"
+        assert "self-check failed" in sh.combine_report()
+        _sums_vs_unsharded(sh)
+    finally:
+        sh.close()
+
+
+def test_rccl_gather_failure_at_run_time_falls_back_to_copies():
+    from shyft_amd.region import SHARD_RCCL_ALWAYS, SHARD_TEST_FAIL_GATHER
+    sh = _flagged(SHARD_RCCL_ALWAYS | SHARD_TEST_FAIL_GATHER)
+    try:
+        assert sh.combine_path() == "rccl" and "self-check passed" in sh.combine_report()
+        _sums_vs_unsharded(sh)                                       # the first all-gather fails: copies, same sums
+        assert sh.combine_path() == "copy"
+        assert "failed at run time" in sh.combine_report()
+    finally:
+        sh.close()
+
+
+def test_shards_on_distinct_gpus_use_rccl():
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    sh = _region("pt_gs_k", [0, 1])
+    try:
+        assert sh.combine_path() == "rccl", sh.combine_report()
+        _sums_vs_unsharded(sh)
+        assert sh.combine_path() == "rccl"
+    finally:
+        sh.close()
+
+
+def test_duplicate_catchments_in_filter_accepted_like_unsharded():
+    ref, sh = _region("pt_gs_k", None), _region("pt_gs_k", [0, 0])
+    try:
+        for r in (ref, sh):
+            r.set_catchment_filter([3, 3, 3, 60])
+            _run(r)
+        cid = synthetic.geo11(N, n_catchments=C)[:, 4]
+        on = np.isin(cid, [3, 60])
+        assert _same(sh.get_series(0, 0, T)[:, on], ref.get_series(0, 0, T)[:, on])
+        assert _same(sh.catchment_sums(0, 0, T), ref.catchment_sums(0, 0, T))
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_shards_below_the_small_region_threshold_equal_unsharded():
+    """262,144 cells = 1,024 workgroups of 256: the unsharded region runs the 4-wave 256-lane pt_gs_k instance, each of
+    its two 131,072-cell shards (512 workgroups <= 2 per CU) the small-region 64-lane speculative instance. The
+    per-cell arithmetic is the same, so every series must be bit-equal (January: Brent jobs on both paths)."""
+    n, Tn = 1 << 18, 96
+    ref, sh = _region("pt_gs_k", None, n=n, T_=Tn), _region("pt_gs_k", [0, 0], n=n, T_=Tn)
+    try:
+        for r in (ref, sh):
+            r.synthetic_forcing(synthetic.SEED, 0, Tn)
+            r.run_cells(0, 0, Tn)
+        for k in range(8):
+            assert _same(sh.get_series(k, 0, Tn), ref.get_series(k, 0, Tn)), f"series {k}"
+        assert _same(sh.get_state(), ref.get_state())
+    finally:
+        ref.close()
+        sh.close()
+
+
+def test_sample_cells_equals_full_series():
+    ref, sh = _region("pt_gs_k", None), _region("pt_gs_k", [0, 0, 0])
+    try:
+        _run(ref)
+        _run(sh)
+        cells = [0, 1, 1365, 1366, 2047, 2048, 4095, 7]
+        full = ref.get_series(1, 0, T)
+        for r in (ref, sh):
+            assert _same(r.sample_cells(1, cells, 10, 40), full[10:50][:, cells])
+            from shyft_amd.region import SERIES_FORCING
+            assert _same(r.sample_cells(SERIES_FORCING + 0, cells, 0, T), ref.get_forcing(0, 0, T)[:, cells])
+        with pytest.raises(RuntimeError, match="out of range"):
+            sh.sample_cells(0, [N], 0, 1)
+    finally:
+        ref.close()
+        sh.close()

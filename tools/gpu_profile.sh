@@ -28,6 +28,8 @@ run write --kernel-trace --pmc WRITE_SIZE
 run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE
 cd $R
 echo "$ARGS" > $O/bench_args.txt
+# build identity of the library these passes measured (bench.py only uses a summary with the same sha)
+python3 -c "from shyft_amd import _native; print(_native.lib_sha())" > $O/lib_sha.txt || exit 1
 echo "$KERNEL" > $O/kernel.txt
 # the summary is written here after the call (profiles/ does not travel back from the box):
 #   python3 tools/pmc_summary.py --kernel $KERNEL --round $ROUND --bench-args "$ARGS" --base $O

@@ -60,7 +60,7 @@ def mean(v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="ptgsk_run_kernel")
-    ap.add_argument("--round", default="r02")
+    ap.add_argument("--round", default="r05")
     ap.add_argument("--bench-args", default="--gpus 1 --steps 20 --warmup 5")
     ap.add_argument("--base", default=os.path.join(ROOT, "gpurun_out"))
     o = ap.parse_args()
@@ -103,7 +103,13 @@ def main():
     timed = launches[W:]
     tr = trace_durations(os.path.join(o.base, "prof_trace", "run_kernel_trace.csv"), o.kernel)
     algo = cells * chunk * (read_b + write_b) + cells * state_b
+    sha_path = os.path.join(o.base, "lib_sha.txt")
+    if not os.path.exists(sha_path):
+        raise SystemExit(f"{sha_path} missing: the passes must record the sha256 of the library they measured "
+                         "(tools/gpu_profile.sh)")
+    lib_sha = open(sha_path).read().strip()
     res = {
+        "lib_sha256": lib_sha,
         "command": f"python3 bench.py {o.bench_args} under rocprofv3 (tools/gpu_profile.sh: one --kernel-trace "
                    f"--stats pass, then one --pmc pass per counter group, each a fresh run of the same command)",
         "workload": bench.workload_tag(a, cells),
