@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--shards", type=int, default=0,
                     help="engine path: shards of the region (default: one per GPU); more shards than GPUs share "
                          "devices round-robin (on one GPU: --gpus 1 --shards 2 runs two shards on device 0)")
+    ap.add_argument("--balance-z", action="store_true",
+                    help="engine shards dealt by elevation rank (SHYFT_HIP_SHARD_BALANCE_Z) instead of contiguous ranges")
     ap.add_argument("--steps", type=int, default=YEAR // CHUNK)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cells", type=int, default=0,
@@ -280,11 +282,12 @@ class Layout:
             self.scaling = "weak"
 
 
-def build_region(stack, L, local, chunk, n_steps_axis, devices=None):
+def build_region(stack, L, local, chunk, n_steps_axis, devices=None, shard_flags=0):
     from shyft_amd import synthetic
     from shyft_amd.region import HipRegion, PT_GS_K, HBV_STACK, PT_SS_K, PT_HS_K, PT_HPS_K, COLLECT_DISCHARGE
     sid = {"pt_gs_k": PT_GS_K, "hbv_stack": HBV_STACK, "pt_ss_k": PT_SS_K, "pt_hs_k": PT_HS_K, "pt_hps_k": PT_HPS_K}[stack]
-    r = HipRegion(sid, L.n, device=local) if devices is None else HipRegion(sid, L.n, devices=devices)
+    r = (HipRegion(sid, L.n, device=local) if devices is None else
+         HipRegion(sid, L.n, devices=devices, shard_flags=shard_flags))
     r.set_geo(synthetic.geo11(L.n, n_catchments=L.n_catch, cell_offset=L.off, n_total=L.total))
     r.set_parameters(stack_defaults(stack, 1)[0])
     r.set_time_axis(synthetic.T0_2015_US, synthetic.HOUR_US, n_steps_axis, chunk)
@@ -601,7 +604,8 @@ def main():
     cells = L.total // n_dev if devices else L.n      # per GPU (the shards of one GPU run concurrently)
     chunk = a.chunk
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
-    r = build_region(a.stack, L, local, chunk, n_axis, devices)
+    from shyft_amd.region import SHARD_BALANCE_Z
+    r = build_region(a.stack, L, local, chunk, n_axis, devices, SHARD_BALANCE_Z if a.balance_z else 0)
     state0 = stack_defaults(a.stack, L.n)[1]
     read_b, write_b, state_b, kernel_name = STACKS[a.stack]
     stations = None
@@ -692,6 +696,7 @@ def main():
         "kernel_ms_per_step": avg_kernel_ms,
         "kernel_cell_steps_per_s": L.total * chunk / (avg_kernel_ms * 1e-3),
         "chunk_wall_ms": [round(w, 2) for w in walls],
+        **({"shard_kernel_ms_last_chunk": [round(x, 2) for x in r.shard_run_ms()]} if devices else {}),
         "chunk_kernel_ms": [round(k, 2) for k in kernel_ms],
         "roofline": {
             "bound": "hbm",

@@ -86,10 +86,16 @@ int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* device
  * time switches the region to device copies (same results; shyft_hip_region_combine_report says why). No reference
  * counterpart: the reference's one-process region has no exchange (core/region_model.h:972-1021).
  * SHYFT_HIP_SHARD_NO_RCCL: device copies only. The TEST_ flags inject the failures for the fallback tests:
- * ncclCommInitAll failing, the first all-gather after the self-check failing, the self-check comparing unequal. */
+ * ncclCommInitAll failing, the first all-gather after the self-check failing, the self-check comparing unequal.
+ * SHYFT_HIP_SHARD_BALANCE_Z: instead of contiguous cell ranges, the first shyft_hip_set_geo ranks the cells by
+ * elevation and deals rank r to shard r % n_shards (each shard keeps its cells in region order), so every shard holds
+ * the same mix of elevations and so of snow-season work. Every entry point still takes the region's cell indexes;
+ * results per cell are unchanged, catchment sums are partial sums added in shard order (each catchment now spans the
+ * shards, so they are reassociated), and shyft_hip_region_shards reports shard k's cell count (cell0 is then only its
+ * position in the deal). */
 enum shyft_hip_shard_flags {
     SHYFT_HIP_SHARD_RCCL_ALWAYS = 1, SHYFT_HIP_SHARD_NO_RCCL = 2, SHYFT_HIP_SHARD_TEST_FAIL_INIT = 4,
-    SHYFT_HIP_SHARD_TEST_FAIL_GATHER = 8, SHYFT_HIP_SHARD_TEST_CORRUPT_CHECK = 16
+    SHYFT_HIP_SHARD_TEST_FAIL_GATHER = 8, SHYFT_HIP_SHARD_TEST_CORRUPT_CHECK = 16, SHYFT_HIP_SHARD_BALANCE_Z = 32
 };
 int shyft_hip_region_create_sharded_ex(int stack, size_t n_cells, const int* devices, size_t n_shards, unsigned flags,
                                        shyft_hip_region** out);
@@ -224,6 +230,9 @@ double shyft_hip_last_run_ms(const shyft_hip_region* h);
    a sharded region: the slowest running shard's). Fills ms[0..min(n, parts)) and returns the number of parts.
    (No reference counterpart: measurement only.) */
 int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n);
+/* Kernel milliseconds of the last run_cells of every shard (0 for a shard idle under the catchment filter) into
+   ms[0..min(n, shards)); returns the number of shards (1 and the region's own time when unsharded). */
+size_t shyft_hip_shard_run_ms(const shyft_hip_region* h, double* ms, size_t n);
 
 /* Response series for steps [step0, step0+n), [n][n_cells]. */
 int shyft_hip_get_series(const shyft_hip_region* h, int series, size_t step0, size_t n, double* dst, int dst_on_device);
@@ -264,6 +273,19 @@ int shyft_hip_cell_series(shyft_hip_region* h, int series, size_t cell, size_t s
  * dst[n][n_cells]. One gather on the device (per shard for a sharded region). */
 int shyft_hip_sample_cells(const shyft_hip_region* h, int series, const int64_t* cells, size_t n_cells, size_t step0,
                            size_t n, double* dst);
+
+/* Test knobs (no reference counterpart; every knob is 0 in production). SHYFT_HIP_KNOB_PTGSK_INSTANCE: 0 = the
+ * launcher picks the pt_gs_k kernel instance by region size, 2 = the 64-lane 2-wave instance, 4 = the 256-lane 4-wave
+ * instance. SHYFT_HIP_KNOB_BRENT_READ_DELAY: n > 0 makes every wavefront of a 256-lane pt_gs_k workgroup except the
+ * first sleep n x s_sleep(127) between the Brent phase and reading its results, so the first wavefront runs ahead
+ * into the next step's job queue (the interleaving the queue's double buffering must survive). */
+enum shyft_hip_knob {
+    SHYFT_HIP_KNOB_PTGSK_INSTANCE = 1, SHYFT_HIP_KNOB_BRENT_READ_DELAY = 2,
+    /* sharded regions: 1 = run_cells runs the shards one after another (per-shard kernel times without contention,
+     * shyft_hip_shard_run_ms); 0 = concurrently (the default) */
+    SHYFT_HIP_KNOB_SERIAL_SHARDS = 3
+};
+int shyft_hip_set_test_knob(shyft_hip_region* h, int knob, int64_t value);
 
 /* region_model::is_cell_env_ts_ok (core/region_model.h:954-962): *ok = 1 when no forcing value of a
  * calculated cell (catchment filter) in the resident window is NaN. */

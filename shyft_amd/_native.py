@@ -57,6 +57,7 @@ SIGNATURES = {
     "shyft_hip_synchronize": (C.c_int, [_h]),
     "shyft_hip_last_run_ms": (C.c_double, [_h]),
     "shyft_hip_last_run_kernel_ms": (C.c_int, [_h, C.c_void_p, C.c_int]),
+    "shyft_hip_shard_run_ms": (C.c_size_t, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_prefetch_synthetic_forcing": (C.c_int, [_h, C.c_uint64, C.c_uint64, C.c_size_t, C.c_int]),
     "shyft_hip_swap_forcing_window": (C.c_int, [_h, C.c_size_t]),
     "shyft_hip_get_series": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
@@ -70,6 +71,7 @@ SIGNATURES = {
     "shyft_hip_region_clone": (C.c_int, [_h, C.POINTER(C.c_void_p)]),
     "shyft_hip_cell_series": (C.c_int, [_h, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),
     "shyft_hip_sample_cells": (C.c_int, [_h, C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p]),
+    "shyft_hip_set_test_knob": (C.c_int, [_h, C.c_int, C.c_int64]),
     "shyft_hip_forcing_ok": (C.c_int, [_h, C.POINTER(C.c_int)]),
     "shyft_hip_set_routing_groups": (C.c_int, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_routing_group_sums": (C.c_int, [_h, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int]),

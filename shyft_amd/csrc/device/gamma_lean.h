@@ -1,0 +1,161 @@
+// The incomplete gamma of gamma_snow (boost gamma_p with the digits10<5>/<10> policy, gamma_snow.h:189-201, as
+// detmath::gamma_pq restates it) in fewer instructions, for the fast domain -- shape a > 0, x positive normal,
+// |a log x - x - lgamma(a)| <= 708 -- where it is bit-identical to detmath::gamma_pq<dev_math>:
+//  - exp and log are inline (detmath's |x| <= 708 / positive-normal fast paths), their polynomial constants read
+//    once from a constant table into SGPRs and used as SGPR operands of v_fma_f64 (gs_fma_s), no call;
+//  - the series and the continued fraction run without their 2^-200 rescale test: with a > 0 the series'
+//    E = (a+1)...(a+n) only grows, so a final E <= 2^200/... proves no term rescaled; the fraction's largest |P| is
+//    kept with a max (no per-term branch) and checked after the loop. An evaluation that would have rescaled, or
+//    that leaves the fast domain, is redone by the general detmath evaluation.
+// Used by the Brent job of device/gs_brent.h (its f) and by calc_snow_state (device/ptgsk_dev.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "special.h"
+
+namespace shyft_dev {
+
+// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: 2/25 .. 2/3, LN2_HI LN2_LO
+static __constant__ double gsb_const[32] = {
+    1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
+    1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
+    2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04, 1.3888888888888889e-03,
+    8.3333333333333333e-03, 4.1666666666666664e-02, 1.6666666666666666e-01,
+    2.0 / 25, 2.0 / 23, 2.0 / 21, 2.0 / 19, 2.0 / 17, 2.0 / 15, 2.0 / 13, 2.0 / 11, 2.0 / 9, 2.0 / 7, 2.0 / 5,
+    2.0 / 3, 0.0, 0.0, 0.0, 0.0, 0.0};
+
+typedef __attribute__((address_space(4))) const double gsb_cdouble;
+
+// a * b + c with c an SGPR pair (wave-uniform constant): one v_fma_f64, no v_mov of the constant
+__device__ __forceinline__ double gs_fma_s(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+
+struct gsb_k {
+    double c[27];
+};
+
+__device__ __forceinline__ gsb_k gsb_load() {
+    const gsb_cdouble* __restrict__ p = (const gsb_cdouble*)gsb_const;
+    asm volatile("" : "+s"(p));  // keep the table opaque: scalar loads into SGPRs, not folded literals
+    gsb_k k;
+#pragma unroll
+    for (int i = 0; i < 27; ++i) k.c[i] = p[i];
+    return k;
+}
+
+// detmath::exp for |x| <= 708 (exp_poly + one ldexp)
+__device__ __forceinline__ double gsb_exp(double x, const gsb_k& k) {
+    const double t = x * k.c[0] + k.c[1];
+    const double kf = t - k.c[1];
+    double r = __builtin_fma(-kf, k.c[2], x);
+    r = __builtin_fma(-kf, k.c[3], r);
+    double p = gs_fma_s(r, k.c[4], k.c[5]);
+#pragma unroll
+    for (int i = 6; i <= 14; ++i) p = gs_fma_s(p, r, k.c[i]);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)kf);
+}
+
+// detmath::log for positive normal finite x (log_dd without its subnormal branch, hi part)
+__device__ __forceinline__ double gsb_log(double x, const gsb_k& k) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    int e = (int)((u >> 52) & 0x7ff) - 1023;
+    double m = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        e += 1;
+    }
+    const double f = m - 1.0;
+    const double d = 2.0 + f;
+    const double d_lo = (2.0 - d) + f;
+    const double s = f / d;
+    const double s_lo = (__builtin_fma(-s, d, f) - s * d_lo) / d;
+    const double z = s * s;
+    double t = gs_fma_s(k.c[15], z, k.c[16]);
+#pragma unroll
+    for (int i = 17; i <= 26; ++i) t = gs_fma_s(t, z, k.c[i]);
+    const double tail = (s * z) * t;
+    const double ed = (double)e;
+    const double a_hi = ed * k.c[2];
+    const double a_lo = ed * k.c[3];
+    const double b = 2.0 * s;
+    const double sum = a_hi + b;
+    const double bb = sum - a_hi;
+    const double err = (a_hi - (sum - bb)) + (b - bb);
+    const double small = ((err + 2.0 * s_lo) + tail) + a_lo;
+    return sum + small;
+}
+
+// P(a, x), P(a+1, x) and the prefix by detmath::gamma_pq's series / continued fraction for the fast domain;
+// ok = false: the caller takes the general evaluation (the value returned is then meaningless)
+__device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, double lga, double eps, double ap1,
+                                                       const gsb_k& k, bool& ok) {
+    const double lx = gsb_log(x, k);
+    const double arg = a * lx - x - lga;
+    ok = a > 0.0 && x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308 && __builtin_fabs(arg) <= 708.0;
+    const double prefix = gsb_exp(arg, k);
+    gamma_p_result r;
+    r.prefix = prefix;
+    r.p = r.p1 = 0.0;
+    if (!ok) return r;  // (x = inf or NaN would not converge: no loop for a lane outside the domain)
+    if (x < ap1) {
+        // series (detmath::gamma_series_sums without the rescale test)
+        double ap = a, E = 1.0, B = 0.0, xn = 1.0;
+        for (int n = 1; n <= 2000; ++n) {
+            ap = ap + 1.0;
+            xn = xn * x;
+            E = E * ap;
+            B = __builtin_fma(B, ap, xn);
+            if (xn < eps * (B + E)) break;
+        }
+        ok = ok && E <= detmath::GPQ_SCALE_HI;
+        const double aE = a * E;
+        const double pp = prefix * ((B + E) / aE);
+        const double pp1 = prefix * (B / aE);
+        r.p = pp < 1.0 ? pp : 1.0;
+        r.p1 = pp1 < 1.0 ? pp1 : 1.0;
+    } else {
+        // continued fraction (detmath::gamma_cf_terms; the rescale test folded into the largest |P|)
+        double bcf = x + 1.0 - a;
+        double Pm = 1.0, Qm = 0.0, P = bcf, Qd = 1.0, di = 0.0, bigP = 0.0;
+        for (int i = 1; i <= 2000; ++i) {
+            di = di + 1.0;
+            const double an = -di * (di - a);
+            bcf = bcf + 2.0;
+            const double Pn = __builtin_fma(bcf, P, an * Pm);
+            const double Qn = __builtin_fma(bcf, Qd, an * Qm);
+            const double cross = Pn * Qd;
+            const double diff = cross - P * Qn;
+            Pm = P; Qm = Qd;
+            P = Pn; Qd = Qn;
+            if (__builtin_fabs(diff) <= eps * __builtin_fabs(cross)) break;
+            bigP = __builtin_fmax(bigP, __builtin_fabs(P));  // NaN P: no rescale there either
+        }
+        ok = ok && !(bigP > detmath::GPQ_SCALE_HI);
+        const double q = prefix * (Qd / P);
+        const double q1 = q + prefix / a;
+        const double pp = 1.0 - q;
+        const double pp1 = 1.0 - q1;
+        r.p = pp > 0.0 ? pp : 0.0;
+        r.p1 = pp1 > 0.0 ? pp1 : 0.0;
+    }
+    return r;
+}
+
+// gs_gamma_pq (device/special.h) by the lean evaluation, the general one where it does not apply; out of line
+// (one copy, its own register budget)
+__device__ __noinline__ gamma_p_result gs_gamma_pq_lean(double a, double x, double lga) {
+    const gsb_k k = gsb_load();
+    const double eps = detmath::gamma_snow_policy_eps(a);
+    bool ok;
+    const gamma_p_result r = gsb_gamma_pq(a, x, lga, eps, a + 1.0, k, ok);
+    if (ok) return r;
+    return gamma_p_prefix(a, x, lga, eps);
+}
+
+}  // namespace shyft_dev

@@ -18,137 +18,16 @@
 #include <hip/hip_runtime.h>
 
 #include "ptgsk_dev.h"
+#include "gamma_lean.h"
 
 namespace shyft_dev {
 
-// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: 2/25 .. 2/3, LN2_HI LN2_LO
-static __constant__ double gsb_const[32] = {
-    1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
-    1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
-    2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04, 1.3888888888888889e-03,
-    8.3333333333333333e-03, 4.1666666666666664e-02, 1.6666666666666666e-01,
-    2.0 / 25, 2.0 / 23, 2.0 / 21, 2.0 / 19, 2.0 / 17, 2.0 / 15, 2.0 / 13, 2.0 / 11, 2.0 / 9, 2.0 / 7, 2.0 / 5,
-    2.0 / 3, 0.0, 0.0, 0.0, 0.0, 0.0};
-
-typedef __attribute__((address_space(4))) const double gsb_cdouble;
-
-// a * b + c with c an SGPR pair (wave-uniform constant): one v_fma_f64, no v_mov of the constant
-__device__ __forceinline__ double gs_fma_s(double a, double b, double c) {
-    double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
-    return d;
-}
-
-struct gsb_k {
-    double c[27];
-};
-
-__device__ __forceinline__ gsb_k gsb_load() {
-    const gsb_cdouble* __restrict__ p = (const gsb_cdouble*)gsb_const;
-    asm volatile("" : "+s"(p));  // keep the table opaque: scalar loads into SGPRs, not folded literals
-    gsb_k k;
-#pragma unroll
-    for (int i = 0; i < 27; ++i) k.c[i] = p[i];
-    return k;
-}
-
-// detmath::exp for |x| <= 708 (exp_poly + one ldexp)
-__device__ __forceinline__ double gsb_exp(double x, const gsb_k& k) {
-    const double t = x * k.c[0] + k.c[1];
-    const double kf = t - k.c[1];
-    double r = __builtin_fma(-kf, k.c[2], x);
-    r = __builtin_fma(-kf, k.c[3], r);
-    double p = gs_fma_s(r, k.c[4], k.c[5]);
-#pragma unroll
-    for (int i = 6; i <= 14; ++i) p = gs_fma_s(p, r, k.c[i]);
-    p = __builtin_fma(p, r, 0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
-    return __builtin_ldexp(p, (int)kf);
-}
-
-// detmath::log for positive normal finite x (log_dd without its subnormal branch, hi part)
-__device__ __forceinline__ double gsb_log(double x, const gsb_k& k) {
-    const uint64_t u = (uint64_t)__double_as_longlong(x);
-    int e = (int)((u >> 52) & 0x7ff) - 1023;
-    double m = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
-    if (m > 1.4142135623730951) {
-        m = m * 0.5;
-        e += 1;
-    }
-    const double f = m - 1.0;
-    const double d = 2.0 + f;
-    const double d_lo = (2.0 - d) + f;
-    const double s = f / d;
-    const double s_lo = (__builtin_fma(-s, d, f) - s * d_lo) / d;
-    const double z = s * s;
-    double t = gs_fma_s(k.c[15], z, k.c[16]);
-#pragma unroll
-    for (int i = 17; i <= 26; ++i) t = gs_fma_s(t, z, k.c[i]);
-    const double tail = (s * z) * t;
-    const double ed = (double)e;
-    const double a_hi = ed * k.c[2];
-    const double a_lo = ed * k.c[3];
-    const double b = 2.0 * s;
-    const double sum = a_hi + b;
-    const double bb = sum - a_hi;
-    const double err = (a_hi - (sum - bb)) + (b - bb);
-    const double small = ((err + 2.0 * s_lo) + tail) + a_lo;
-    return sum + small;
-}
-
-// calc_q(a, b, z) = a b P(a+1, z/b) + z (1 - P(a, z/b)) for the fast domain; ok = false: take gs_calc_q
+// calc_q(a, b, z) = a b P(a+1, z/b) + z (1 - P(a, z/b)) for the fast domain (device/gamma_lean.h); ok = false:
+// take gs_calc_q
 __device__ __forceinline__ double gsb_calc_q(double a, double b, double z, double lga, double eps, double ap1,
                                              const gsb_k& k, bool& ok) {
-    const double x = z / b;
-    const double lx = gsb_log(x, k);
-    const double arg = a * lx - x - lga;
-    ok = x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308 && __builtin_fabs(arg) <= 708.0;
-    const double prefix = gsb_exp(arg, k);
-    double p, p1;
-    if (x < ap1) {
-        // series (detmath::gamma_series_sums without the rescale test: see the header)
-        double ap = a, E = 1.0, B = 0.0, xn = 1.0;
-        for (int n = 1; n <= 2000; ++n) {
-            ap = ap + 1.0;
-            xn = xn * x;
-            E = E * ap;
-            B = __builtin_fma(B, ap, xn);
-            if (xn < eps * (B + E)) break;
-        }
-        ok = ok && E <= detmath::GPQ_SCALE_HI;
-        const double aE = a * E;
-        const double pp = prefix * ((B + E) / aE);
-        const double pp1 = prefix * (B / aE);
-        p = pp < 1.0 ? pp : 1.0;
-        p1 = pp1 < 1.0 ? pp1 : 1.0;
-    } else {
-        // continued fraction (detmath::gamma_cf_terms, the rescale test folded into a flag)
-        double bcf = x + 1.0 - a;
-        double Pm = 1.0, Qm = 0.0, P = bcf, Qd = 1.0, di = 0.0;
-        bool big = false;
-        for (int i = 1; i <= 2000; ++i) {
-            di = di + 1.0;
-            const double an = -di * (di - a);
-            bcf = bcf + 2.0;
-            const double Pn = __builtin_fma(bcf, P, an * Pm);
-            const double Qn = __builtin_fma(bcf, Qd, an * Qm);
-            const double cross = Pn * Qd;
-            const double diff = cross - P * Qn;
-            Pm = P; Qm = Qd;
-            P = Pn; Qd = Qn;
-            if (__builtin_fabs(diff) <= eps * __builtin_fabs(cross)) break;
-            big = big || __builtin_fabs(P) > detmath::GPQ_SCALE_HI;
-        }
-        ok = ok && !big;
-        const double q = prefix * (Qd / P);
-        const double q1 = q + prefix / a;
-        const double pp = 1.0 - q;
-        const double pp1 = 1.0 - q1;
-        p = pp > 0.0 ? pp : 0.0;
-        p1 = pp1 > 0.0 ? pp1 : 0.0;
-    }
-    return a * b * p1 + z * (1.0 - p);
+    const gamma_p_result g = gsb_gamma_pq(a, z / b, lga, eps, ap1, k, ok);
+    return a * b * g.p1 + z * (1.0 - g.p);
 }
 
 // the general evaluation, out of line (rare: Q1 without the opening state's gamma pair, or a lane outside the
@@ -307,6 +186,20 @@ __device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1,
 __device__ __noinline__ double gs_corr_lwc_memo(double z1, double a1, double b1, double a2, double b2, double q1,
                                                 double lga2, const gsb_memo& memo) {
     return gs_corr_lwc_lean_t<true>(z1, a1, b1, a2, b2, q1, lga2, &memo);
+}
+
+// the memo of the workgroup-wide speculative opening (kernels/ptgsk.hip): f at the four opening points of the job
+// at fz[0..3] (LDS, written by four lanes of any wavefront before the solve); the points themselves are recomputed
+// here by the same function, so the memo needs no LDS of its own
+__device__ __noinline__ double gs_corr_lwc_memo4(double z1, double a1, double b1, double a2, double b2, double q1,
+                                                 double lga2, const double* fz) {
+    gsb_memo mm;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        mm.z[k] = gs_brent_point(z1, k);
+        mm.f[k] = fz[k];
+    }
+    return gs_corr_lwc_lean_t<true>(z1, a1, b1, a2, b2, q1, lga2, &mm);
 }
 
 }  // namespace shyft_dev

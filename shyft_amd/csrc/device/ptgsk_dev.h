@@ -13,6 +13,7 @@
 
 #include "pt_dev.h"
 #include "special.h"
+#include "gamma_lean.h"
 #include "../include_internal/layout.h"
 
 
@@ -55,6 +56,12 @@ struct gs_lw {
     double p = __builtin_nan(""), p1 = __builtin_nan("");
 };
 
+// calc_snow_state's incomplete gamma: the lean out-of-line evaluation (device/gamma_lean.h; the general one where it
+// does not apply). 1M cells, the year in 730-step chunks: 92.7 -> 91.6 ms per chunk, bit-exact (r05 variants)
+__device__ __forceinline__ gamma_p_result gs_gamma_pq_cs(double a, double x, double lga) {
+    return gs_gamma_pq_lean(a, x, lga);
+}
+
 // gamma_snow.h:230-260
 template <class LGC>
 __device__ inline void calc_snow_state(double shape, double scale, double y0, double lambda, double lwd,
@@ -71,7 +78,7 @@ __device__ inline void calc_snow_state(double shape, double scale, double y0, do
         return;
     } else {
         const double x = lambda / scale;
-        const gamma_p_result g = gs_gamma_pq(shape, x, lgc.get(shape));
+        const gamma_p_result g = gs_gamma_pq_cs(shape, x, lgc.get(shape));
         y = g.p;
         y1 = y - g.prefix / shape;
         swe = m * (1.0 - y1) - lambda * (1 - y);
@@ -82,7 +89,7 @@ __device__ inline void calc_snow_state(double shape, double scale, double y0, do
     else if (lwd > 0.0) {
         const double sat = lwd / max_water_frac;
         const double x = sat / scale;
-        const gamma_p_result g = gs_gamma_pq(shape, x, lgc.get(shape));
+        const gamma_p_result g = gs_gamma_pq_cs(shape, x, lgc.get(shape));
         lw.p = g.p;
         lw.p1 = g.p1;
         const double ssa = g.p;

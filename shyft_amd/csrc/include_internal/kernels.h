@@ -29,6 +29,11 @@ struct ptgsk_kargs {
     double* state_series;          // [PTGSK_NS][win_len+1][N] or null
     const uint8_t* active;         // [N] catchment filter or null
     int32_t* err;                  // [N]
+    // test knobs (shyft_hip_set_test_knob; 0 in production): instance 2 / 4 forces the 64-lane 2-wave or the 256-lane
+    // 4-wave instance; read_delay > 0 makes every wavefront but the first sleep read_delay x s_sleep(127) after the
+    // Brent phase's second barrier, before reading its lanes' results (forces the job-queue interleaving)
+    int instance;
+    int read_delay;
 };
 
 hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream);
@@ -107,14 +112,15 @@ struct routing_args {
 };
 hipError_t launch_route(const routing_args& a, const int* level_off, int n_levels, hipStream_t stream);
 
-// synthetic workload generator, fills [5][n][N] window rows
+// synthetic workload generator, fills [5][n][N] window rows; cell i is generator cell
+// cell_offset + (ids ? ids[i] : i) (ids: a z-balanced shard's region cells, shards.hip)
 // few-workgroup, non-temporal-store variant for generating beside a running kernel (n_blocks workgroups)
 hipError_t launch_synthetic_forcing_stream(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                            uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
-                                           int n_blocks, hipStream_t stream);
+                                           int n_blocks, hipStream_t stream, const int64_t* ids = nullptr);
 hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                     uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
-                                    hipStream_t stream);
+                                    hipStream_t stream, const int64_t* ids = nullptr);
 
 // sums over selected cells: out[t] = sum_k w[k]*series[t][cells[k]] for t in [0,n)
 // (w == null -> plain sum), deterministic fixed-order tree per step

@@ -65,6 +65,7 @@ struct shyft_hip_region {
     hipEvent_t ev_copy = nullptr;  // shyft_hip_copy_state: the copy out of this region's state has finished
     std::string err;
     double last_ms = 0.0;
+    int knob_instance = 0, knob_read_delay = 0;  // shyft_hip_set_test_knob (pt_gs_k launches)
 
     // host mirrors
     std::vector<double> geo;  // n x 11
@@ -98,6 +99,7 @@ struct shyft_hip_region {
     dbuf<int64_t> d_trel;
     dbuf<uint8_t> d_active;
     dbuf<double> d_tmp, d_w, d_alt;
+    dbuf<int64_t> d_cell_ids;  // a z-balanced shard: the region cell of each of its cells (synthetic forcing keys)
     dbuf<int32_t> d_flag;
 
     // inverse-distance neighbour tables, one per forcing variable, cached by

@@ -11,6 +11,9 @@ shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_
                             unsigned flags);  // throws
 void shard_set_destroy(shard_set* s);
 
+// region.hip: the generator keys of a region's cells (null: 0..n-1), for a z-balanced shard
+void region_set_cell_ids(shyft_hip_region* h, const int64_t* ids);  // throws
+
 // region.hip: sum over the selected cells of one region (select_cells semantics), value x cell area when weighted;
 // *sum_area = the selected cells' area sum (weighted only). dst[n] host. No selection match: dst = 0.
 int region_selected_sums(shyft_hip_region* h, int series, const int64_t* ids, size_t n_ids, int scope, int weighted,
@@ -20,6 +23,8 @@ namespace shards {
 size_t info(const shard_set* s, size_t k, int* device, size_t* cell0, size_t* n_cells);
 int combine_path(const shard_set* s);
 const char* combine_report(const shard_set* s);
+void set_test_knob(shard_set* s, int knob, int64_t value);
+size_t shard_run_ms(const shard_set* s, double* ms, size_t n);
 void sample_cells(shard_set* s, int series, const int64_t* cells, size_t n_cells, size_t step0, size_t n, double* dst);
 void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double* rdist);
 void set_parameters(shard_set* s, const double* params, size_t n_sets, size_t n_per_set, const int32_t* set_ix);

@@ -47,7 +47,15 @@ extern "C" int shyft_ptgsk_prof_read(unsigned long long* out) {
 
 namespace {
 
-constexpr int BLOCK = 256;
+#ifndef SHYFT_PTGSK_BIG_B
+#define SHYFT_PTGSK_BIG_B 256
+#endif
+constexpr int BLOCK = SHYFT_PTGSK_BIG_B;
+// SPEC4: the speculative Brent opening over the whole workgroup in the large-region instance (4 lanes of any
+// wavefront per job, the f values in jres, the solve itself on the first wavefront)
+#ifndef SHYFT_PTGSK_SPEC4
+#define SHYFT_PTGSK_SPEC4 0
+#endif
 
 #ifndef SHYFT_LB_WAVES
 #define SHYFT_LB_WAVES 4
@@ -250,7 +258,21 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                 // the speculative opening when the jobs' point lanes fit the solving wavefront: 4 lanes per job
                 // (z1, u1, u2a, u2b: two f rounds saved) or 2 (z1, u1: one round saved)
                 const int L = SPEC ? (4 * nj <= 64 ? 4 : 2 * nj <= 64 ? 2 : 0) : 0;
-                if (L) {
+                if (!SPEC && SHYFT_PTGSK_SPEC4 && 4 * nj <= B && nj <= 64) {
+                    // every wavefront evaluates opening points (4 lanes per job); f values into jres
+                    const int jj = t >> 2;
+                    if (jj < nj) {
+                        const gsb_zf r = gs_corr_lwc_spec(jz1[jj], ja1[jj], jb1[jj], ja2[jj], jb2[jj], jq1[jj], jlg2[jj], t & 3);
+                        jres[t] = r.f;
+                    }
+                    __syncthreads();
+                    // the solving lanes are all in the first wavefront (nj <= 64): each reads its four memo values
+                    // inside the call, before any of them writes its result over the memo below
+                    if (t < nj) {
+                        const double res = gs_corr_lwc_memo4(jz1[t], ja1[t], jb1[t], ja2[t], jb2[t], jq1[t], jlg2[t], &jres[4 * t]);
+                        jres[t] = res;
+                    }
+                } else if (L) {
                     const int jj = L == 4 ? t >> 2 : t >> 1;
                     if (t < 64 && jj < nj) {
                         const gsb_zf r = gs_corr_lwc_spec(jz1[jj], ja1[jj], jb1[jj], ja2[jj], jb2[jj], jq1[jj], jlg2[jj], t & (L - 1));
@@ -274,6 +296,10 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                 __builtin_amdgcn_s_setprio(0);
 #endif
                 __syncthreads();
+                // test knob: the other wavefronts read their results late, so a fast first wavefront is already
+                // enqueueing the next step's jobs (jres must not alias the job arrays for this to stay exact)
+                if (a.read_delay > 0 && (threadIdx.x >> 6) != 0)
+                    for (int k = 0; k < a.read_delay; ++k) __builtin_amdgcn_s_sleep(127);
                 if (slot >= 0) z = jres[slot];
             }
         }
@@ -391,7 +417,7 @@ hipError_t launch_ptgsk_run(const ptgsk_kargs& a, hipStream_t stream) {
         }
     }
     static const char* force = getenv("SHYFT_PTGSK_WAVES");  // measurement knob: "2" / "4" forces an instance
-    const bool small = force ? force[0] == '2' : grid <= 2 * n_cu;
+    const bool small = a.instance ? a.instance == 2 : force ? force[0] == '2' : grid <= 2 * n_cu;
     if (a.n_cells < 0)  // never (n_cells > 0): keeps ptgsk_callee_budget_kernel in the module
         hipLaunchKernelGGL(ptgsk_callee_budget_kernel, dim3(1), dim3(BLOCK), 0, stream, a);
     if (a.fcol) {

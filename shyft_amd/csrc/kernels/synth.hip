@@ -16,12 +16,13 @@ namespace {
 __global__ __launch_bounds__(256) void synthetic_forcing_stream_kernel(double* __restrict__ forcing, size_t win_len,
                                                                        size_t row0, size_t n_rows, size_t n_cells,
                                                                        uint64_t seed, uint64_t cell_offset,
-                                                                       uint64_t step0, const double* __restrict__ zc) {
+                                                                       uint64_t step0, const double* __restrict__ zc,
+                                                                       const int64_t* __restrict__ ids) {
 #pragma clang fp contract(off)
     for (size_t cell = blockIdx.x * (size_t)blockDim.x + threadIdx.x; cell < n_cells;
          cell += (size_t)gridDim.x * blockDim.x) {
         const double z = zc[cell];
-        const uint64_t gcell = cell_offset + cell;
+        const uint64_t gcell = cell_offset + (ids ? (uint64_t)ids[cell] : cell);
         for (size_t r = 0; r < n_rows; ++r) {
             double v[5];
             synth_values(seed, gcell, step0 + r, z, v);
@@ -34,12 +35,13 @@ __global__ __launch_bounds__(256) void synthetic_forcing_stream_kernel(double* _
 __global__ __launch_bounds__(256) void synthetic_forcing_kernel(double* __restrict__ forcing, size_t win_len, size_t row0,
                                                                 size_t n_rows, size_t n_cells, uint64_t seed,
                                                                 uint64_t cell_offset, uint64_t step0,
-                                                                const double* __restrict__ zc) {
+                                                                const double* __restrict__ zc,
+                                                                const int64_t* __restrict__ ids) {
 #pragma clang fp contract(off)
     const size_t cell = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (cell >= n_cells) return;
     const double z = zc[cell];
-    const uint64_t gcell = cell_offset + cell;
+    const uint64_t gcell = cell_offset + (ids ? (uint64_t)ids[cell] : cell);
     for (size_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
         const uint64_t step = step0 + r;
         double v[5];
@@ -53,22 +55,22 @@ __global__ __launch_bounds__(256) void synthetic_forcing_kernel(double* __restri
 
 hipError_t launch_synthetic_forcing(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                     uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, const int64_t* ids) {
     if (n_rows == 0 || n_cells == 0) return hipSuccess;
     const unsigned gx = (unsigned)((n_cells + 255) / 256);
     unsigned gy = (unsigned)(n_rows < 64 ? n_rows : 64);
     hipLaunchKernelGGL(synthetic_forcing_kernel, dim3(gx, gy), dim3(256), 0, stream, forcing, win_len, row0, n_rows,
-                       n_cells, seed, cell_offset, step0, z);
+                       n_cells, seed, cell_offset, step0, z, ids);
     return hipGetLastError();
 }
 
 hipError_t launch_synthetic_forcing_stream(double* forcing, size_t win_len, size_t row0, size_t n_rows, size_t n_cells,
                                            uint64_t seed, uint64_t cell_offset, uint64_t step0, const double* z,
-                                           int n_blocks, hipStream_t stream) {
+                                           int n_blocks, hipStream_t stream, const int64_t* ids) {
     if (n_rows == 0 || n_cells == 0) return hipSuccess;
     const size_t need = (n_cells + 255) / 256;
     const unsigned gx = (unsigned)(need < (size_t)n_blocks ? need : (size_t)n_blocks);
     hipLaunchKernelGGL(synthetic_forcing_stream_kernel, dim3(gx), dim3(256), 0, stream, forcing, win_len, row0, n_rows,
-                       n_cells, seed, cell_offset, step0, z);
+                       n_cells, seed, cell_offset, step0, z, ids);
     return hipGetLastError();
 }

@@ -715,7 +715,7 @@ int shyft_hip_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uint64_t cel
         if (!h->has_geo) throw std::runtime_error("synthetic_forcing: geo_cell_data not set");
         const double* z = h->d_alt.p;
         hip_check(launch_synthetic_forcing(h->d_forcing.p, h->TW, step0 - h->w0, n, h->n, seed, cell_offset, step0, z,
-                                           h->stream),
+                                           h->stream, h->d_cell_ids.p),
                   "synthetic_forcing");
         hip_check(hipStreamSynchronize(h->stream), "sync");
     });
@@ -759,7 +759,7 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
         hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_gen, 0), "wait");
         const int blocks = 4 * (n_cus > 0 ? n_cus : 256);  // 4 workgroups of 4 waves per CU (grid-stride over cells)
         hip_check(launch_synthetic_forcing_stream(h->d_forcing_next.p, h->TW, 0, h->TW, h->n, seed, cell_offset,
-                                                  w0_next, h->d_alt.p, blocks, h->gen_stream),
+                                                  w0_next, h->d_alt.p, blocks, h->gen_stream, h->d_cell_ids.p),
                   "synthetic_forcing (prefetch)");
         hip_check(hipEventRecord(h->ev_gen, h->gen_stream), "record");
         h->gen_w0 = w0_next;
@@ -1150,6 +1150,8 @@ static void launch_run(shyft_hip_region* h, int start_step, int n_steps) {
     a.state_series = h->collect_state ? h->d_state_series.p : nullptr;
     a.active = h->active.empty() ? nullptr : h->d_active.p;
     a.err = h->d_err.p;
+    a.instance = h->knob_instance;
+    a.read_delay = h->knob_read_delay;
     hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
     hip_check(launch_ptgsk_run(a, h->stream), "ptgsk_run_kernel launch");
     hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
@@ -1235,6 +1237,13 @@ int shyft_hip_synchronize(shyft_hip_region* h) {
 
 double shyft_hip_last_run_ms(const shyft_hip_region* h) { return h ? (h->sh ? shards::last_run_ms(h->sh) : h->last_ms) : 0.0; }
 
+size_t shyft_hip_shard_run_ms(const shyft_hip_region* h, double* ms, size_t n) {
+    if (!h) return 0;
+    if (h->sh) return shards::shard_run_ms(h->sh, ms, n);
+    if (n > 0 && ms) ms[0] = h->last_ms;
+    return 1;
+}
+
 int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n) {
     if (!h) return 0;
     if (h->sh) return shards::last_run_kernel_ms(h->sh, ms, n);
@@ -1271,6 +1280,16 @@ int shyft_hip_get_state_series(const shyft_hip_region* hc, int field, size_t ste
 
 }  // extern "C"
 namespace shyft_hip_impl {
+void region_set_cell_ids(shyft_hip_region* h, const int64_t* ids) {
+    if (!ids) {
+        h->d_cell_ids.release();
+        return;
+    }
+    hip_check(hipSetDevice(h->device), "hipSetDevice");
+    h->d_cell_ids.alloc(h->n);
+    hip_check(region_copy(h, h->d_cell_ids.p, ids, h->n * sizeof(int64_t), hipMemcpyHostToDevice), "upload cell ids");
+}
+
 int region_selected_sums(shyft_hip_region* h, int series, const int64_t* ids, size_t n_ids, int scope, int weighted,
                          size_t step0, size_t n, double* dst, double* sum_area_out, size_t* n_selected) {
     return guarded(h, [&] {
@@ -1418,6 +1437,7 @@ int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out) 
         clone_buf(h->d_seg_off, src->d_seg_off);
         clone_buf(h->d_active, src->d_active);
         clone_buf(h->d_alt, src->d_alt);
+        clone_buf(h->d_cell_ids, src->d_cell_ids);
     });
     if (rc) {
         g_last_error = h->err;
@@ -1465,6 +1485,25 @@ int shyft_hip_sample_cells(const shyft_hip_region* hc, int series, const int64_t
         h->d_tmp.alloc(std::max(h->d_tmp.n, n * n_cells));
         hip_check(launch_gather_columns(h->d_tmp.p, rows, n, h->n, h->d_sel.p, n_cells, h->stream), "gather_columns");
         copy_rows(h->stream, dst, h->d_tmp.p, n * n_cells * sizeof(double), 0, 1);
+    });
+}
+
+int shyft_hip_set_test_knob(shyft_hip_region* h, int knob, int64_t value) {
+    if (!h) return fail(h, "shyft_hip_set_test_knob: null handle");
+    if (h->sh) return guarded(h, [&] { shards::set_test_knob(h->sh, knob, value); });
+    return guarded(h, [&] {
+        if (knob == SHYFT_HIP_KNOB_PTGSK_INSTANCE) {
+            if (value != 0 && value != 2 && value != 4)
+                throw std::runtime_error("set_test_knob: pt_gs_k instance must be 0 (auto), 2 or 4");
+            h->knob_instance = int(value);
+        } else if (knob == SHYFT_HIP_KNOB_SERIAL_SHARDS) {
+            throw std::runtime_error("set_test_knob: serial shards needs a sharded region");
+        } else if (knob == SHYFT_HIP_KNOB_BRENT_READ_DELAY) {
+            if (value < 0 || value > 1000) throw std::runtime_error("set_test_knob: read delay must be in [0, 1000]");
+            h->knob_read_delay = int(value);
+        } else {
+            throw std::runtime_error("set_test_knob: unknown knob");
+        }
     });
 }
 

@@ -55,11 +55,27 @@ struct shard_set {
     std::string report;                // how the combine path was chosen, its self-check, run-time fallbacks
     bool gather_fail_armed = false;    // SHYFT_HIP_SHARD_TEST_FAIL_GATHER: the next all-gather fails
     size_t ens_members = 0;
+    // SHYFT_HIP_SHARD_BALANCE_Z: the cells are dealt to the shards by elevation rank (fixed at the first set_geo), so
+    // every shard holds the same mix of elevations; each shard keeps its cells in region order
+    bool serial = false;                       // SHYFT_HIP_KNOB_SERIAL_SHARDS: run_cells one shard after another
+    bool permuted = false;
+    std::vector<std::vector<int64_t>> cells;   // permuted: region cells of shard k, ascending
+    std::vector<int32_t> cell_k, cell_j;       // permuted: region cell -> (shard, index in the shard)
 
     size_t S() const { return r.size(); }
-    size_t shard_of(size_t cell) const {
-        return size_t(std::upper_bound(b.begin(), b.end(), cell) - b.begin()) - 1;
+    size_t nk(size_t k) const { return e[k] - b[k]; }
+    // shard and index in the shard of a region cell
+    void locate(size_t cell, size_t& k, size_t& j) const {
+        if (permuted) {
+            k = size_t(cell_k[cell]);
+            j = size_t(cell_j[cell]);
+        } else {
+            k = size_t(std::upper_bound(b.begin(), b.end(), cell) - b.begin()) - 1;
+            j = cell - b[k];
+        }
     }
+    // region cell of index j of shard k
+    int64_t cell_at(size_t k, size_t j) const { return permuted ? cells[k][j] : int64_t(b[k] + j); }
 };
 
 namespace {
@@ -97,13 +113,39 @@ void for_shards(shard_set* s, F&& f, bool parallel = true) {
         if (!errs[k].empty()) throw std::runtime_error(errs[k]);
 }
 
-// rows of a [n][N] host array <-> the [n][n_k] block of shard k
-void split_cols(const double* src, size_t N, size_t n, size_t b, size_t nk, std::vector<double>& dst) {
+// columns of a [n][N] host array <-> the [n][n_k] block of shard k
+void split_cols(const shard_set* s, const double* src, size_t n, size_t k, std::vector<double>& dst) {
+    const size_t N = s->n, nk = s->nk(k);
     dst.resize(n * nk);
-    for (size_t t = 0; t < n; ++t) std::copy(src + t * N + b, src + t * N + b + nk, dst.begin() + t * nk);
+    if (!s->permuted) {
+        for (size_t t = 0; t < n; ++t) std::copy(src + t * N + s->b[k], src + t * N + s->e[k], dst.begin() + t * nk);
+        return;
+    }
+    const std::vector<int64_t>& c = s->cells[k];
+    for (size_t t = 0; t < n; ++t)
+        for (size_t j = 0; j < nk; ++j) dst[t * nk + j] = src[t * N + size_t(c[j])];
 }
-void join_cols(const std::vector<double>& src, size_t N, size_t n, size_t b, size_t nk, double* dst) {
-    for (size_t t = 0; t < n; ++t) std::copy(src.begin() + t * nk, src.begin() + (t + 1) * nk, dst + t * N + b);
+void join_cols(const shard_set* s, const std::vector<double>& src, size_t n, size_t k, double* dst) {
+    const size_t N = s->n, nk = s->nk(k);
+    if (!s->permuted) {
+        for (size_t t = 0; t < n; ++t)
+            std::copy(src.begin() + t * nk, src.begin() + (t + 1) * nk, dst + t * N + s->b[k]);
+        return;
+    }
+    const std::vector<int64_t>& c = s->cells[k];
+    for (size_t t = 0; t < n; ++t)
+        for (size_t j = 0; j < nk; ++j) dst[t * N + size_t(c[j])] = src[t * nk + j];
+}
+// rows of a [N][width] host array of shard k's cells: a pointer into src (contiguous shards) or a gathered copy
+template <class T>
+const T* shard_rows(const shard_set* s, size_t k, const T* src, size_t width, std::vector<T>& tmp) {
+    if (!src) return nullptr;
+    if (!s->permuted) return src + s->b[k] * width;
+    const std::vector<int64_t>& c = s->cells[k];
+    tmp.resize(c.size() * width);
+    for (size_t j = 0; j < c.size(); ++j) std::copy(src + size_t(c[j]) * width, src + (size_t(c[j]) + 1) * width,
+                                                     tmp.begin() + j * width);
+    return tmp.data();
 }
 
 void drop_comms(shard_set* s) {
@@ -341,8 +383,15 @@ shard_set* shard_set_create(int stack, size_t n_cells, const int* devices, size_
     // every per-shard vector is complete before any shard resource exists, so a failure part-way (a shard that
     // cannot be allocated) unwinds through shard_set_destroy with consistent indexes
     for (size_t k = 0; k < n_shards; ++k) {
-        s->b.push_back(n_cells * k / n_shards);
-        s->e.push_back(n_cells * (k + 1) / n_shards);
+        if (flags & SHYFT_HIP_SHARD_BALANCE_Z) {
+            // the deal of shyft_hip_set_geo (rank r -> shard r % S) gives the first n % S shards one cell more
+            const size_t q = n_cells / n_shards, rem = n_cells % n_shards;
+            s->b.push_back(k * q + std::min(k, rem));
+            s->e.push_back(s->b.back() + q + (k < rem ? 1 : 0));
+        } else {
+            s->b.push_back(n_cells * k / n_shards);
+            s->e.push_back(n_cells * (k + 1) / n_shards);
+        }
         s->dev.push_back(devices[k]);
         s->idle.push_back(0);
     }
@@ -390,10 +439,57 @@ int combine_path(const shard_set* s) { return s->path; }
 
 const char* combine_report(const shard_set* s) { return s->report.c_str(); }
 
+void set_test_knob(shard_set* s, int knob, int64_t value) {
+    if (knob == SHYFT_HIP_KNOB_SERIAL_SHARDS) {
+        s->serial = value != 0;
+        return;
+    }
+    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_set_test_knob(s->r[k], knob, value)); }, false);
+}
+
+size_t shard_run_ms(const shard_set* s, double* ms, size_t n) {
+    for (size_t k = 0; k < s->S() && k < n; ++k) ms[k] = s->idle[k] ? 0.0 : shyft_hip_last_run_ms(s->r[k]);
+    return s->S();
+}
+
+// SHYFT_HIP_SHARD_BALANCE_Z: rank the cells by elevation (geo z, ties and NaN by cell index) and deal rank r to
+// shard r % S, so that every shard gets every S-th cell of the elevation order. Snow-season cost grows with elevation
+// (more snow, more corr_lwc Brent jobs: gamma_snow.h:425-435), and real regions hold their catchments -- and so their
+// elevations -- in contiguous cell blocks, which contiguous shards would hand to one device each.
+void deal_by_elevation(shard_set* s, const double* geo11) {
+    const size_t N = s->n, S = s->S();
+    std::vector<int64_t> order(N);
+    for (size_t i = 0; i < N; ++i) order[i] = int64_t(i);
+    auto z = [&](int64_t i) { return geo11[size_t(i) * 11 + 2]; };
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        const double za = z(a), zb = z(b);
+        if (za != za || zb != zb) return zb != zb && za == za;  // NaN last
+        return za < zb;
+    });
+    s->cells.assign(S, {});
+    for (size_t r = 0; r < N; ++r) s->cells[r % S].push_back(order[r]);
+    s->cell_k.assign(N, 0);
+    s->cell_j.assign(N, 0);
+    for (size_t k = 0; k < S; ++k) {
+        std::sort(s->cells[k].begin(), s->cells[k].end());
+        if (s->cells[k].size() != s->nk(k)) throw std::runtime_error("set_geo: elevation deal does not match the shard sizes");
+        for (size_t j = 0; j < s->cells[k].size(); ++j) {
+            s->cell_k[size_t(s->cells[k][j])] = int32_t(k);
+            s->cell_j[size_t(s->cells[k][j])] = int32_t(j);
+        }
+    }
+    s->permuted = true;
+    for_shards(s, [&](size_t k) { region_set_cell_ids(s->r[k], s->cells[k].data()); });
+}
+
 void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double* rdist) {
+    // the deal is fixed by the first geometry (later set_geo calls keep it: a layout, not a result)
+    if ((s->flags & SHYFT_HIP_SHARD_BALANCE_Z) && !s->permuted) deal_by_elevation(s, geo11);
     for_shards(s, [&](size_t k) {
-        ck(s->r[k], shyft_hip_set_geo(s->r[k], geo11 + s->b[k] * 11, rid ? rid + s->b[k] : nullptr,
-                                      rdist ? rdist + s->b[k] : nullptr));
+        std::vector<double> g, d;
+        std::vector<int64_t> id;
+        ck(s->r[k], shyft_hip_set_geo(s->r[k], shard_rows(s, k, geo11, 11, g), shard_rows(s, k, rid, 1, id),
+                                      shard_rows(s, k, rdist, 1, d)));
     });
     map_catchments(s, geo11);
     std::fill(s->idle.begin(), s->idle.end(), 0);  // set_geo clears the filter state of each shard
@@ -401,7 +497,8 @@ void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double
 
 void set_parameters(shard_set* s, const double* params, size_t n_sets, size_t n_per_set, const int32_t* set_ix) {
     for_shards(s, [&](size_t k) {
-        ck(s->r[k], shyft_hip_set_parameters(s->r[k], params, n_sets, n_per_set, set_ix ? set_ix + s->b[k] : nullptr));
+        std::vector<int32_t> ix;
+        ck(s->r[k], shyft_hip_set_parameters(s->r[k], params, n_sets, n_per_set, shard_rows(s, k, set_ix, 1, ix)));
     });
 }
 
@@ -441,15 +538,29 @@ void set_catchment_filter(shard_set* s, const int64_t* cids, size_t n) {
 }
 
 void set_state(shard_set* s, const double* state, size_t n_fields) {
-    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_set_state(s->r[k], state + s->b[k] * n_fields, n_fields)); });
+    for_shards(s, [&](size_t k) {
+        std::vector<double> rows;
+        ck(s->r[k], shyft_hip_set_state(s->r[k], shard_rows(s, k, state, n_fields, rows), n_fields));
+    });
 }
 
 void get_state(shard_set* s, double* state, size_t n_fields) {
-    for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_get_state(s->r[k], state + s->b[k] * n_fields, n_fields)); });
+    for_shards(s, [&](size_t k) {
+        if (!s->permuted) {
+            ck(s->r[k], shyft_hip_get_state(s->r[k], state + s->b[k] * n_fields, n_fields));
+            return;
+        }
+        std::vector<double> rows(s->nk(k) * n_fields);
+        ck(s->r[k], shyft_hip_get_state(s->r[k], rows.data(), n_fields));
+        for (size_t j = 0; j < s->nk(k); ++j)
+            std::copy(rows.begin() + j * n_fields, rows.begin() + (j + 1) * n_fields,
+                      state + size_t(s->cells[k][j]) * n_fields);
+    });
 }
 
 void copy_state(shard_set* d, const shard_set* src) {
-    if (d->S() != src->S() || d->b != src->b) throw std::runtime_error("copy_state: regions are sharded differently");
+    if (d->S() != src->S() || d->b != src->b || d->permuted != src->permuted || d->cells != src->cells)
+        throw std::runtime_error("copy_state: regions are sharded differently");
     for_shards(d, [&](size_t k) { ck(d->r[k], shyft_hip_copy_state(d->r[k], src->r[k])); });
 }
 
@@ -457,7 +568,7 @@ void set_forcing(shard_set* s, int var, size_t step0, size_t n, const double* sr
     if (on_device) throw std::runtime_error("set_forcing: a sharded region takes forcing from host memory");
     for_shards(s, [&](size_t k) {
         std::vector<double> blk;
-        split_cols(src, s->n, n, s->b[k], s->e[k] - s->b[k], blk);
+        split_cols(s, src, n, k, blk);
         ck(s->r[k], shyft_hip_set_forcing(s->r[k], var, step0, n, blk.data(), 0));
     });
 }
@@ -466,13 +577,13 @@ void set_forcing(shard_set* s, int var, size_t step0, size_t n, const double* sr
 void get_rows(shard_set* s, int what, int id, size_t step0, size_t n, double* dst, int on_device) {
     if (on_device) throw std::runtime_error("a sharded region returns series to host memory");
     for_shards(s, [&](size_t k) {
-        const size_t nk = s->e[k] - s->b[k];
+        const size_t nk = s->nk(k);
         std::vector<double> blk(n * nk);
         shyft_hip_region* c = s->r[k];
         ck(c, what == 0   ? shyft_hip_get_forcing(c, id, step0, n, blk.data(), 0)
               : what == 1 ? shyft_hip_get_series(c, id, step0, n, blk.data(), 0)
                           : shyft_hip_get_state_series(c, id, step0, n, blk.data(), 0));
-        join_cols(blk, s->n, n, s->b[k], nk, dst);
+        join_cols(s, blk, n, k, dst);
     });
 }
 
@@ -507,13 +618,16 @@ void interpolate_btk(shard_set* s, size_t n_sources, const double* xyz, const do
 
 void synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n) {
     for_shards(s, [&](size_t k) {
-        ck(s->r[k], shyft_hip_synthetic_forcing(s->r[k], seed, cell_offset + s->b[k], step0, n));
+        // generator cell of shard cell j: cell_offset + its region cell (contiguous: b[k] + j; dealt: the shard's
+        // cell ids, region_set_cell_ids)
+        ck(s->r[k], shyft_hip_synthetic_forcing(s->r[k], seed, cell_offset + (s->permuted ? 0 : s->b[k]), step0, n));
     });
 }
 
 void prefetch_synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t w0_next, int n_cus) {
     for_shards(s, [&](size_t k) {
-        ck(s->r[k], shyft_hip_prefetch_synthetic_forcing(s->r[k], seed, cell_offset + s->b[k], w0_next, n_cus));
+        ck(s->r[k], shyft_hip_prefetch_synthetic_forcing(s->r[k], seed, cell_offset + (s->permuted ? 0 : s->b[k]),
+                                                         w0_next, n_cus));
     });
 }
 
@@ -525,7 +639,7 @@ void swap_forcing_window(shard_set* s, size_t w0_next) {
 void run_cells(shard_set* s, size_t use_ncore, int start_step, int n_steps) {
     for_shards(s, [&](size_t k) {
         if (!s->idle[k]) ck(s->r[k], shyft_hip_run_cells(s->r[k], use_ncore, start_step, n_steps));
-    });
+    }, !s->serial);
 }
 
 void run_cells_async(shard_set* s, int start_step, int n_steps) {
@@ -562,9 +676,10 @@ int last_run_kernel_ms(const shard_set* s, double* ms, int n) {
 
 void cell_series(shard_set* s, int series, size_t cell, size_t step0, size_t n, double* buf, int write) {
     if (cell >= s->n) throw std::runtime_error("cell_series: cell index out of range");
-    const size_t k = s->shard_of(cell);
+    size_t k, j;
+    s->locate(cell, k, j);
     hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
-    ck(s->r[k], shyft_hip_cell_series(s->r[k], series, cell - s->b[k], step0, n, buf, write));
+    ck(s->r[k], shyft_hip_cell_series(s->r[k], series, j, step0, n, buf, write));
 }
 
 // columns of selected cells: each shard gathers the ones it holds, into their columns of dst [n][n_cells]
@@ -573,8 +688,9 @@ void sample_cells(shard_set* s, int series, const int64_t* cells, size_t m, size
     std::vector<std::vector<size_t>> col(s->S());
     for (size_t j = 0; j < m; ++j) {
         if (cells[j] < 0 || size_t(cells[j]) >= s->n) throw std::runtime_error("sample_cells: cell index out of range");
-        const size_t k = s->shard_of(size_t(cells[j]));
-        loc[k].push_back(cells[j] - int64_t(s->b[k]));
+        size_t k, jj;
+        s->locate(size_t(cells[j]), k, jj);
+        loc[k].push_back(int64_t(jj));
         col[k].push_back(j);
     }
     for_shards(s, [&](size_t k) {
@@ -610,8 +726,9 @@ void statistics(shard_set* s, int series, const int64_t* ids, size_t n_ids, int 
                     throw std::runtime_error("Supplied cell index reference " + std::to_string(ids[j]) +
                                              " is ouside valid range 0 .." + std::to_string(s->n));
                 if (ids[j] == int64_t(s->n)) continue;  // valid index, no cell (the reference's range check is <=)
-                const size_t k = s->shard_of(size_t(ids[j]));
-                sel[k].push_back(ids[j] - int64_t(s->b[k]));
+                size_t k, jj;
+                s->locate(size_t(ids[j]), k, jj);
+                sel[k].push_back(int64_t(jj));
                 any[k] = 1;
             } else {
                 if (s->cid_to_cix.count(ids[j]) == 0)
@@ -674,7 +791,8 @@ void catchment_ids(const shard_set* s, int64_t* cids) {
 
 void set_routing_groups(shard_set* s, const int32_t* group_of_cell, size_t n_groups) {
     for_shards(s, [&](size_t k) {
-        ck(s->r[k], shyft_hip_set_routing_groups(s->r[k], group_of_cell ? group_of_cell + s->b[k] : nullptr, n_groups));
+        std::vector<int32_t> g;
+        ck(s->r[k], shyft_hip_set_routing_groups(s->r[k], shard_rows(s, k, group_of_cell, 1, g), n_groups));
     });
     s->n_groups = n_groups;
 }
@@ -737,6 +855,10 @@ shard_set* clone(const shard_set* src) {
     s->child_cids = src->child_cids;
     s->n_groups = src->n_groups;
     s->flags = src->flags & ~unsigned(SHYFT_HIP_SHARD_TEST_FAIL_GATHER);
+    s->permuted = src->permuted;   // (the shard regions' cell ids are cloned with them)
+    s->cells = src->cells;
+    s->cell_k = src->cell_k;
+    s->cell_j = src->cell_j;
     for (size_t k = 0; k < src->S(); ++k) {
         hip_check(hipSetDevice(src->dev[k]), "hipSetDevice");
         shyft_hip_region* c = nullptr;

@@ -27,8 +27,10 @@ HBV_STATE = (("swe", "sca", "soil_moisture", "tank_uz", "tank_lz", "n_bins") +
              tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) + tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
 SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
 SERIES_FORCING, SERIES_STATE = 100, 200
+KNOB_PTGSK_INSTANCE, KNOB_BRENT_READ_DELAY, KNOB_SERIAL_SHARDS = 1, 2, 3
 # shyft_hip_region_create_sharded_ex options (include/shyft_hip.h)
 SHARD_RCCL_ALWAYS, SHARD_NO_RCCL, SHARD_TEST_FAIL_INIT, SHARD_TEST_FAIL_GATHER, SHARD_TEST_CORRUPT_CHECK = 1, 2, 4, 8, 16
+SHARD_BALANCE_Z = 32
 # pt_ss_k (core/pt_ss_k.h:154-181, pt_ss_k_cell_model.h:38-200); response series ids are the pt_gs_k ones
 PTSSK_STATE = ("nu", "alpha", "sca", "swe", "free_water", "residual", "num_units", "kirchner_q")
 PTSSK_STATE_SERIES = ("kirchner_discharge", "snow_sca", "snow_swe", "snow_alpha", "snow_nu", "snow_lwc",
@@ -228,6 +230,12 @@ class HipRegion:
         n = self._L.shyft_hip_last_run_kernel_ms(self.h, buf, 4)
         return [float(buf[k]) for k in range(n)]
 
+    def shard_run_ms(self) -> list:
+        """Kernel ms of every shard's last run_cells (one entry when unsharded)."""
+        buf = (C.c_double * 256)()
+        n = int(self._L.shyft_hip_shard_run_ms(self.h, buf, 256))
+        return [float(buf[k]) for k in range(min(n, 256))]
+
     def get_series(self, series: int, step0: int, n: int) -> np.ndarray:
         out = np.empty((n, self.n), dtype=np.float64)
         self._chk(self._L.shyft_hip_get_series(self.h, series, step0, n, _ptr(out), 0))
@@ -249,6 +257,10 @@ class HipRegion:
         out = np.empty((n, c.size), dtype=np.float64)
         self._chk(self._L.shyft_hip_sample_cells(self.h, int(series), _ptr(c), c.size, int(step0), int(n), _ptr(out)))
         return out
+
+    def set_test_knob(self, knob: int, value: int):
+        """KNOB_PTGSK_INSTANCE (0 auto, 2, 4) / KNOB_BRENT_READ_DELAY (s_sleep(127) rounds); tests only."""
+        self._chk(self._L.shyft_hip_set_test_knob(self.h, int(knob), int(value)))
 
     def statistics(self, series: int, ids=(), scope: int = SCOPE_CATCHMENT, weighted: bool = False, step0: int = 0,
                    n: int | None = None) -> np.ndarray:

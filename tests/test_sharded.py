@@ -344,3 +344,65 @@ def test_sample_cells_equals_full_series():
     finally:
         ref.close()
         sh.close()
+
+
+# ---- SHYFT_HIP_SHARD_BALANCE_Z: shards dealt by elevation rank ("interleave or sort cells by z") ----
+
+def _ramp_region(n, devices, flags=0, T_=438):
+    """pt_gs_k region whose elevation ramps 0 -> 3000 m with the cell index (catchments at rising elevation, as in
+    real regions), January: the high cells carry the snow and the corr_lwc Brent jobs, the low ones do not."""
+    import bench
+    from shyft_amd.region import HipRegion, COLLECT_DISCHARGE
+    r = HipRegion(1, n, devices=devices, shard_flags=flags) if devices is not None else HipRegion(1, n)
+    g = synthetic.geo11(n, n_catchments=C)
+    g[:, 2] = np.linspace(0.0, 3000.0, n)
+    r.set_geo(g)
+    r.set_parameters(bench.stack_defaults("pt_gs_k", 1)[0])
+    r.set_time_axis(synthetic.T0_2015_US, HOUR, T_)
+    r.set_collection(COLLECT_DISCHARGE)
+    r.set_state(bench.stack_defaults("pt_gs_k", n)[1])
+    return r
+
+
+def test_balance_z_spreads_snow_work_and_keeps_results():
+    from shyft_amd.region import SHARD_BALANCE_Z, KNOB_SERIAL_SHARDS
+    n, S, T_ = 1 << 19, 4, 438
+    ref = _ramp_region(n, None, T_=T_)
+    try:
+        ref.synthetic_forcing(synthetic.SEED, 0, T_)
+        ref.run_cells(0, 0, T_)
+        exp = [ref.get_series(k, 0, T_) for k in range(2)]
+        exp_state = ref.get_state()
+        exp_sums = ref.catchment_sums(0, 0, T_)
+    finally:
+        ref.close()
+    spread = {}
+    for name, flags in (("contiguous", 0), ("balanced", SHARD_BALANCE_Z)):
+        sh = _ramp_region(n, [0] * S, flags, T_)
+        try:
+            sh.set_test_knob(KNOB_SERIAL_SHARDS, 1)     # per-shard kernel times without the other shards beside
+            sh.synthetic_forcing(synthetic.SEED, 0, T_)
+            sh.run_cells(0, 0, T_)
+            ms = sh.shard_run_ms()
+            spread[name] = (max(ms) - min(ms)) / max(ms)
+            for k in range(2):                         # per-cell results in the region's cell order: exact
+                assert _same(sh.get_series(k, 0, T_), exp[k]), f"{name} series {k}"
+            assert _same(sh.get_state(), exp_state)
+            a = sh.catchment_sums(0, 0, T_)
+            if flags:                                  # every catchment spans the shards: reassociated
+                assert np.allclose(a, exp_sums, rtol=1e-12, atol=0)
+                cells = [0, 1, n // 2, n - 1, 12345]
+                assert _same(sh.sample_cells(0, cells, 0, T_), exp[0][:, cells])
+                buf = np.empty(T_)
+                from shyft_amd import _native
+                import ctypes as C_
+                assert sh._L.shyft_hip_cell_series(sh.h, 1, n - 1, 0, T_, buf.ctypes.data_as(C_.c_void_p), 0) == 0
+                assert _same(buf, exp[1][:, n - 1])
+                f = sh.get_forcing(1, 0, 4)            # forcing in region order; and back
+                sh.set_forcing(1, 0, f)
+                assert _same(sh.get_forcing(1, 0, 4), f)
+            print(name, [round(x, 2) for x in ms], round(spread[name], 3))
+        finally:
+            sh.close()
+    assert spread["balanced"] <= 0.10, spread
+    assert spread["contiguous"] > 2 * spread["balanced"], spread

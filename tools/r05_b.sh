@@ -4,7 +4,7 @@
 set -o pipefail
 R=$(pwd); mkdir -p gpurun_out
 : > gpurun_out/progress.log
-timeout -k 10 600 python -u -m pytest tests/test_sharded.py -x -v --timeout 300 --timeout-method thread > gpurun_out/t_sharded.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_sharded.py tests/test_brent_interleave.py -x -v --timeout 300 --timeout-method thread > gpurun_out/t_sharded.log 2>&1; rc=$?
 tail -25 gpurun_out/t_sharded.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 1500 python -u -m pytest tests/test_configs_sharded.py -x -v --timeout 1200 --timeout-method thread > gpurun_out/t_configs.log 2>&1; rc=$?
