@@ -203,27 +203,41 @@ def dist_setup(n_gpus, use_gpu=True):
     if world > 1:
         import torch
         import torch.distributed as dist
-        backend = os.environ.get("SHYFT_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+        # GPU ranks: RCCL for device tensors, gloo for host tensors in the same group -- the host path the combines
+        # fall back to if the RCCL self-check below fails (distributed.verify_collectives)
+        backend = os.environ.get("SHYFT_DIST_BACKEND", "cpu:gloo,cuda:nccl" if use_gpu else "gloo")
         if use_gpu:
             # one rank per GPU (RCCL over xGMI). SHYFT_DIST_BACKEND=gloo + more ranks than GPUs is only for
             # rehearsing the multi-rank path on a one-GPU box; the device index wraps in that case.
             n_dev = torch.cuda.device_count()
-            if backend == "nccl" and n_dev < world:
+            if "nccl" in backend and n_dev < world:
                 raise SystemExit(f"bench.py: {world} ranks need {world} GPUs for RCCL, {n_dev} visible "
                                  f"(SHYFT_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
             local = local % n_dev if n_dev else local
             torch.cuda.set_device(local)
-        dist.init_process_group(backend)
+        try:
+            dist.init_process_group(backend)
+        except Exception:  # noqa: BLE001 -- a torch without mixed-backend groups: RCCL alone (no host fallback)
+            if backend != "cpu:gloo,cuda:nccl":
+                raise
+            dist.init_process_group("nccl")
         assert dist.get_world_size() == n_gpus
         pg = dist
+        if use_gpu:
+            # one known-value all-gather, bit-exact on every rank, before any data uses RCCL
+            from shyft_amd import distributed
+            import torch
+            distributed.verify_collectives(device=torch.device("cuda", local))
     return world, rank, local, pg
 
 
 def _backend_name(pg):
     if pg is None:
         return "single rank"
-    b = pg.get_backend()
-    return "RCCL" if b == "nccl" else b
+    from shyft_amd import distributed
+    b = str(pg.get_backend())
+    name = "RCCL" if "nccl" in b and not distributed._COMBINE["host"] else "gloo (host)" if "gloo" in b else b
+    return f"{name}; {distributed.combine_report()}"
 
 
 def barrier_sync(pg, local, devices=None):

@@ -115,7 +115,7 @@ class _HbvBase(_ModelMixin):
         return _Statistics(self, {"output": (8, True)})
 
 
-def _ctor(self, full, args, devices=None):
+def _ctor(self, full, args, devices=None, shard_flags=0):
     base = _api._HbvRegionModel
     if len(args) == 1 and isinstance(args[0], base):
         other = args[0]
@@ -127,22 +127,22 @@ def _ctor(self, full, args, devices=None):
     geo, region_param = args[0], args[1]
     cps = args[2] if len(args) > 2 else {}
     base.__init__(self, list(geo), region_param.to_vector(), {int(k): v.to_vector() for k, v in cps.items()}, full,
-                  [int(d) for d in (devices or [])])
+                  [int(d) for d in (devices or [])], int(shard_flags))
     self._init_python(region_param, cps)
 
 
 class HbvModel(_HbvBase, _api._HbvRegionModel):
     """region_model<hbv_stack cell_complete_response_t> (hbv_stack.cpp:140)."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, True, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, True, args, devices, shard_flags)
 
 
 class HbvOptModel(_HbvBase, _api._HbvRegionModel):
     """region_model<hbv_stack cell_discharge_response_t> (hbv_stack.cpp:141)."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, False, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, False, args, devices, shard_flags)
 
 
 def create_opt_model_clone(src_model):

@@ -87,7 +87,7 @@ class _PTGSKBase(_ModelMixin):
         return _Statistics(self, {"output": (6, True), "pot_ratio": ("pot_ratio", True)})
 
 
-def _ctor(self, base, full, args, devices=None):
+def _ctor(self, base, full, args, devices=None, shard_flags=0):
     if len(args) == 1 and isinstance(args[0], (_api._PTGSKRegionModel,)):
         other = args[0]
         base.__init__(self, other, full)
@@ -98,22 +98,22 @@ def _ctor(self, base, full, args, devices=None):
     geo, region_param = args[0], args[1]
     cps = args[2] if len(args) > 2 else {}
     base.__init__(self, list(geo), region_param.to_vector(), {int(k): v.to_vector() for k, v in cps.items()}, full,
-                  [int(d) for d in (devices or [])])
+                  [int(d) for d in (devices or [])], int(shard_flags))
     self._init_python(region_param, cps)
 
 
 class PTGSKModel(_PTGSKBase, _api._PTGSKRegionModel):
     """region_model<pt_gs_k cell_complete_response_t> (pt_gs_k.cpp:146, all_response_collector)."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, _api._PTGSKRegionModel, True, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, _api._PTGSKRegionModel, True, args, devices, shard_flags)
 
 
 class PTGSKOptModel(_PTGSKBase, _api._PTGSKRegionModel):
     """region_model<pt_gs_k cell_discharge_response_t> (pt_gs_k.cpp:147, discharge_collector)."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, _api._PTGSKRegionModel, False, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, _api._PTGSKRegionModel, False, args, devices, shard_flags)
 
 
 def create_opt_model_clone(src_model, with_catchment_params=False):

@@ -114,7 +114,7 @@ class _PTHPSKBase(_ModelMixin):
         return _Statistics(self, {"output": (6, True), "pot_ratio": ("pot_ratio", True)})
 
 
-def _ctor(self, full, args, devices=None):
+def _ctor(self, full, args, devices=None, shard_flags=0):
     base = _api._PTHPSKRegionModel
     if len(args) == 1 and isinstance(args[0], base):
         other = args[0]
@@ -126,22 +126,22 @@ def _ctor(self, full, args, devices=None):
     geo, region_param = args[0], args[1]
     cps = args[2] if len(args) > 2 else {}
     base.__init__(self, list(geo), region_param.to_vector(), {int(k): v.to_vector() for k, v in cps.items()}, full,
-                  [int(d) for d in (devices or [])])
+                  [int(d) for d in (devices or [])], int(shard_flags))
     self._init_python(region_param, cps)
 
 
 class PTHPSKModel(_PTHPSKBase, _api._PTHPSKRegionModel):
     """region_model<pt_hps_k cell_complete_response_t> (pt_hps_k.cpp models())."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, True, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, True, args, devices, shard_flags)
 
 
 class PTHPSKOptModel(_PTHPSKBase, _api._PTHPSKRegionModel):
     """region_model<pt_hps_k cell_discharge_response_t> (pt_hps_k.cpp models())."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, False, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, False, args, devices, shard_flags)
 
 
 def create_opt_model_clone(src_model):

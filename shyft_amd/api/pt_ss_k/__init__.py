@@ -74,7 +74,7 @@ class _PTSSKBase(_ModelMixin):
         return _Statistics(self, {"output": (6, True), "pot_ratio": ("pot_ratio", True)})
 
 
-def _ctor(self, full, args, devices=None):
+def _ctor(self, full, args, devices=None, shard_flags=0):
     base = _api._PTSSKRegionModel
     if len(args) == 1 and isinstance(args[0], base):
         other = args[0]
@@ -86,22 +86,22 @@ def _ctor(self, full, args, devices=None):
     geo, region_param = args[0], args[1]
     cps = args[2] if len(args) > 2 else {}
     base.__init__(self, list(geo), region_param.to_vector(), {int(k): v.to_vector() for k, v in cps.items()}, full,
-                  [int(d) for d in (devices or [])])
+                  [int(d) for d in (devices or [])], int(shard_flags))
     self._init_python(region_param, cps)
 
 
 class PTSSKModel(_PTSSKBase, _api._PTSSKRegionModel):
     """region_model<pt_ss_k cell_complete_response_t> (pt_ss_k.cpp:139)."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, True, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, True, args, devices, shard_flags)
 
 
 class PTSSKOptModel(_PTSSKBase, _api._PTSSKRegionModel):
     """region_model<pt_ss_k cell_discharge_response_t> (pt_ss_k.cpp:140)."""
 
-    def __init__(self, *args, devices=None):
-        _ctor(self, False, args, devices)
+    def __init__(self, *args, devices=None, shard_flags=0):
+        _ctor(self, False, args, devices, shard_flags)
 
 
 def create_opt_model_clone(src_model):

@@ -31,13 +31,14 @@ template <class Stack>
 void bind_model(py::module_& m, const char* name) {
     using M = region_model<Stack>;
     py::class_<M>(m, name, py::dynamic_attr())
-        .def(py::init<const std::vector<geo_cell_data>&, const std::vector<double>&, bool, int, const std::vector<int>&>(),
+        .def(py::init<const std::vector<geo_cell_data>&, const std::vector<double>&, bool, int, const std::vector<int>&,
+                      unsigned>(),
              py::arg("geo_data_vector"), py::arg("region_param"), py::arg("full_collection") = true,
-             py::arg("device") = -1, py::arg("devices") = std::vector<int>())
+             py::arg("device") = -1, py::arg("devices") = std::vector<int>(), py::arg("shard_flags") = 0u)
         .def(py::init<const std::vector<geo_cell_data>&, const std::vector<double>&,
-                      const std::map<int64_t, std::vector<double>>&, bool, const std::vector<int>&>(),
+                      const std::map<int64_t, std::vector<double>>&, bool, const std::vector<int>&, unsigned>(),
              py::arg("geo_data_vector"), py::arg("region_param"), py::arg("catchment_parameters"),
-             py::arg("full_collection") = true, py::arg("devices") = std::vector<int>())
+             py::arg("full_collection") = true, py::arg("devices") = std::vector<int>(), py::arg("shard_flags") = 0u)
         .def_property_readonly("shard_devices", &M::shard_devices)
         .def(py::init<const M&, bool>(), py::arg("other_model"), py::arg("full_collection"))
         .def_readwrite("ncore", &M::ncore)

@@ -237,17 +237,19 @@ class region_model {
     using state_t = std::vector<double>;
 
     // region_model(const vector<geo_cell_data>&, const parameter_t&)  (region_model.h:285-293)
-    // devices: the region's cells in contiguous shards, one per entry (repeats allowed), all driven from this process
-    // (shyft_hip_region_create_sharded); empty: one region on `device`
+    // devices: the region's cells in shards, one per entry (repeats allowed), all driven from this process
+    // (shyft_hip_region_create_sharded_ex; shard_flags e.g. SHYFT_HIP_SHARD_BALANCE_Z); empty: one region on `device`
     region_model(const std::vector<geo_cell_data>& geov, const parameter_t& region_param, bool full_collection = true,
-                 int device = -1, const std::vector<int>& devices = {})
+                 int device = -1, const std::vector<int>& devices = {}, unsigned shard_flags = 0)
         : geo_(geov), full_(full_collection) {
         if (geo_.empty()) throw std::runtime_error("region_model: no cells");
         shyft_hip_region* h = nullptr;
         if (devices.empty())
             throw_if(shyft_hip_region_create(Stack::id, geo_.size(), device, &h), nullptr);
         else
-            throw_if(shyft_hip_region_create_sharded(Stack::id, geo_.size(), devices.data(), devices.size(), &h), nullptr);
+            throw_if(shyft_hip_region_create_sharded_ex(Stack::id, geo_.size(), devices.data(), devices.size(),
+                                                        shard_flags, &h),
+                     nullptr);
         h_.reset(h, shyft_hip_region_destroy);
         ncore = std::max(1u, std::thread::hardware_concurrency());
         state_collection_.assign(geo_.size(), false);
@@ -262,8 +264,8 @@ class region_model {
     // region_model(cells, region_param, catchment_parameters)  (region_model.h:294-301)
     region_model(const std::vector<geo_cell_data>& geov, const parameter_t& region_param,
                  const std::map<int64_t, parameter_t>& catchment_parameters, bool full_collection = true,
-                 const std::vector<int>& devices = {})
-        : region_model(geov, region_param, full_collection, -1, devices) {
+                 const std::vector<int>& devices = {}, unsigned shard_flags = 0)
+        : region_model(geov, region_param, full_collection, -1, devices, shard_flags) {
         for (const auto& kv : catchment_parameters) set_catchment_parameter(kv.first, kv.second);
     }
     // copy ctor / clone (region_model.h:297, clone :256-276): a true deep copy, device data included;

@@ -28,13 +28,78 @@ def env_rank() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+# set by verify_collectives: the device collectives failed their self-check (or raised), so every later combine
+# moves its (small) partials through the host backend of the same process group instead
+_COMBINE = {"host": False, "report": "not verified"}
+
+
 def _wire(t, group=None):
     """The tensor the backend can move: RCCL ("nccl") takes device tensors; gloo (the CPU rehearsal
-    backend, also used for more ranks than GPUs on one box) only host tensors."""
+    backend, also used for more ranks than GPUs on one box, and the fallback after a failed RCCL self-check)
+    only host tensors."""
     import torch.distributed as dist
-    if t.is_cuda and dist.get_backend(group) == "gloo":
+    if t.is_cuda and (_COMBINE["host"] or dist.get_backend(group) == "gloo"):
         return t.cpu()
     return t
+
+
+def _known(rank: int, m: int):
+    """m doubles that depend on the rank, signed, spread over 60 binades (every mantissa bit matters)"""
+    import torch
+    j = torch.arange(m, dtype=torch.int64)
+    mant = ((rank * 2654435761 + j * 40503) % 1000003).to(torch.float64) + 0.5
+    mant = torch.where(j % 2 == 1, -mant, mant)
+    return torch.ldexp(mant, (j % 61 - 30).to(torch.float64))
+
+
+def verify_collectives(device=None, group=None, inject_failure: bool = False, m: int = 4096) -> str:
+    """Bit-exact self-check of the all-gather the combines use, before any data goes through it: every rank
+    contributes m known doubles, every rank must receive all of them bit for bit. The ranks agree on the outcome
+    over the host backend (a CPU all-reduce of a flag); if any rank failed (or the collective raised), every later
+    combine_partials / max_over_ranks moves its partials through the host backend instead -- the same values,
+    slower. With a mixed process group ("cpu:gloo,cuda:nccl") that host path needs no second group. Returns the
+    report (also in combine_report()). inject_failure: the fallback test's failure on this rank."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        _COMBINE.update(host=False, report="single rank: nothing to combine")
+        return _COMBINE["report"]
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    ok, why = True, ""
+    try:
+        t = _known(rank, m)
+        if device is not None:
+            t = t.to(device)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)   # every rank enters the collective, failing or not
+        if inject_failure:
+            raise RuntimeError("injected all-gather failure")
+        for r in range(world):
+            got = parts[r].cpu().view(torch.int64)
+            if not torch.equal(got, _known(r, m).view(torch.int64)):
+                ok, why = False, f"rank {rank} received rank {r}'s values with different bits"
+                break
+    except Exception as e:  # noqa: BLE001 -- any failure of the device path means: use the host path
+        ok, why = False, f"{type(e).__name__}: {e}"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    if "gloo" in str(dist.get_backend(group)) or device is None:
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)   # host tensor: the group's CPU backend
+    else:  # a device-only group: agree over the device (no host path to fall back to then)
+        fd = flag.to(device)
+        dist.all_reduce(fd, op=dist.ReduceOp.MIN, group=group)
+        flag = fd.cpu()
+    if int(flag.item()) == 1:
+        kind = "device" if device is not None and getattr(device, "type", "cpu") == "cuda" else "host"
+        _COMBINE.update(host=False, report=f"{kind} all-gather self-check passed ({world} ranks x {m} known doubles "
+                                           f"bit-exact on every rank)")
+    else:
+        _COMBINE.update(host=True, report="host (gloo) combines: the device all-gather self-check failed"
+                                          + (f" on this rank ({why})" if why else " on another rank"))
+    return _COMBINE["report"]
+
+
+def combine_report() -> str:
+    return _COMBINE["report"]
 
 
 def combine_partials(partial, group=None, out=None):

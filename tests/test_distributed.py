@@ -129,3 +129,64 @@ def test_combine_partials_gloo_world2():
     cid = (np.arange(n_cells) * C) // n_cells
     ref = np.stack([series[:, cid == c].sum(axis=1) for c in range(C)])
     assert np.allclose(res[0][1], ref, rtol=1e-13, atol=1e-13)
+
+
+def _verify_worker(rank, world, port, inject_rank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rep = distributed.verify_collectives(inject_failure=(rank == inject_rank))
+        host = distributed._COMBINE["host"]
+        part = torch.from_numpy(np.arange(6, dtype=np.float64).reshape(2, 3) * (rank + 1))
+        total = distributed.combine_partials(part).numpy()
+        q.put((rank, rep, host, total, distributed.max_over_ranks(float(rank))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("inject_rank", [-1, 1])
+def test_collective_self_check_and_host_fallback_gloo_world2(inject_rank):
+    """verify_collectives: the known-value all-gather passes (no injection), or one rank's failure switches EVERY
+    rank to the host path (they agree over the host backend); the combines give the same sums either way."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_verify_worker, args=(r, world, port, inject_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, rep, host, total, mx in res:
+        assert host == (inject_rank >= 0), rep
+        assert ("self-check passed" in rep) == (inject_rank < 0)
+        assert np.array_equal(total, np.arange(6, dtype=np.float64).reshape(2, 3) * 3)
+        assert mx == 1.0
+    if inject_rank >= 0:
+        assert "injected" in res[inject_rank][1] and "another rank" in res[1 - inject_rank][1]
+
+
+@pytest.mark.gpu
+def test_mixed_backend_group_on_the_gpu_box():
+    """bench.py's rank group is "cpu:gloo,cuda:nccl": device tensors over RCCL, host tensors (the self-check's vote
+    and the fallback combines) over gloo. One rank here (RCCL puts one rank per GPU): the group forms, a device
+    all-gather and a host all-reduce both run, and the self-check reports."""
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("cpu:gloo,cuda:nccl", rank=0, world_size=1)
+    try:
+        dev = torch.device("cuda", 0)
+        t = distributed._known(0, 64).to(dev)
+        parts = [torch.empty_like(t)]
+        dist.all_gather(parts, t)
+        assert torch.equal(parts[0].cpu().view(torch.int64), distributed._known(0, 64).view(torch.int64))
+        h = torch.tensor([3], dtype=torch.int64)
+        dist.all_reduce(h, op=dist.ReduceOp.MIN)
+        assert int(h.item()) == 3
+        assert "single rank" in distributed.verify_collectives(device=dev)
+        total = distributed.combine_partials(torch.ones(4, dtype=torch.float64, device=dev))
+        assert total.is_cuda and float(total.sum()) == 4.0
+    finally:
+        dist.destroy_process_group()

@@ -3,6 +3,9 @@
 set -o pipefail
 R=$(pwd); mkdir -p gpurun_out
 : > gpurun_out/progress.log
+timeout -k 10 300 python -u -m pytest tests/test_sharded.py -x -v -s -k balance --timeout 240 --timeout-method thread > gpurun_out/t_balance.log 2>&1; rc=$?
+grep -E "contiguous|balanced|PASS|FAIL|passed|failed" gpurun_out/t_balance.log | tail -6
+[ $rc -eq 0 ] || { tail -30 gpurun_out/t_balance.log; exit $rc; }
 timeout -k 10 1000 python -u -m pytest tests/test_configs_sharded.py -x -v --timeout 900 --timeout-method thread > gpurun_out/t_configs.log 2>&1; rc=$?
 grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/t_configs.log | tail -8; cat gpurun_out/progress.log
 [ $rc -eq 0 ] || { tail -30 gpurun_out/t_configs.log; exit $rc; }

@@ -3,7 +3,7 @@
 # C3 gathers), the 131K-cell shard line, and the C2 line with the generator overlapped (no CU mask).
 set -o pipefail
 R=$(pwd); mkdir -p gpurun_out
-timeout -k 10 300 python tools/ptgsk_variants.py tools/vlib/base.so tools/vlib/b512.so shyft_amd/lib/libshyft_hip.so > gpurun_out/var_e.log 2>&1; rc=$?; cat gpurun_out/var_e.log
+timeout -k 10 300 python tools/ptgsk_variants.py tools/vlib/base.so tools/vlib/b512.so tools/vlib/u2.so tools/vlib/u2b512.so shyft_amd/lib/libshyft_hip.so > gpurun_out/var_e.log 2>&1; rc=$?; cat gpurun_out/var_e.log
 case $rc in 124|134|137|139) exit $rc;; esac
 cd /tmp && export TMPDIR=/tmp
 for v in idw_c idw_g4 idw_g2w3 idw_g4w3 idw_g2w3z idw_g4w4z; do
