@@ -227,7 +227,8 @@ def dist_setup(n_gpus, use_gpu=True):
             # one known-value all-gather, bit-exact on every rank, before any data uses RCCL
             from shyft_amd import distributed
             import torch
-            distributed.verify_collectives(device=torch.device("cuda", local))
+            nccl = "nccl" in str(dist.get_backend())
+            distributed.verify_collectives(device=torch.device("cuda", local) if nccl else None)
     return world, rank, local, pg
 
 

@@ -15,10 +15,6 @@
 
 namespace shyft_dev {
 
-#ifndef SHYFT_GSB_U2
-#define SHYFT_GSB_U2 0
-#endif
-
 // exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: 2/25 .. 2/3, LN2_HI LN2_LO
 static __constant__ double gsb_const[32] = {
     1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
@@ -42,9 +38,9 @@ struct gsb_k {
 };
 
 __device__ __forceinline__ gsb_k gsb_load() {
+    gsb_k k;
     const gsb_cdouble* __restrict__ p = (const gsb_cdouble*)gsb_const;
     asm volatile("" : "+s"(p));  // keep the table opaque: scalar loads into SGPRs, not folded literals
-    gsb_k k;
 #pragma unroll
     for (int i = 0; i < 27; ++i) k.c[i] = p[i];
     return k;
@@ -110,20 +106,6 @@ __device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, doubl
     if (x < ap1) {
         // series (detmath::gamma_series_sums without the rescale test)
         double ap = a, E = 1.0, B = 0.0, xn = 1.0;
-#if SHYFT_GSB_U2
-        // two terms per exit test: the state of the first term whose test fires, as the term-by-term loop
-        for (int n = 1; n < 2000; n += 2) {
-            const double ap1_ = ap + 1.0, xn1 = xn * x, E1 = E * ap1_, B1 = __builtin_fma(B, ap1_, xn1);
-            const double ap2 = ap1_ + 1.0, xn2 = xn1 * x, E2 = E1 * ap2, B2 = __builtin_fma(B1, ap2, xn2);
-            const bool t1 = xn1 < eps * (B1 + E1), t2 = xn2 < eps * (B2 + E2);
-            if (t1 | t2) {
-                B = t1 ? B1 : B2;
-                E = t1 ? E1 : E2;
-                break;
-            }
-            ap = ap2; xn = xn2; E = E2; B = B2;
-        }
-#else
         for (int n = 1; n <= 2000; ++n) {
             ap = ap + 1.0;
             xn = xn * x;
@@ -131,7 +113,6 @@ __device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, doubl
             B = __builtin_fma(B, ap, xn);
             if (xn < eps * (B + E)) break;
         }
-#endif
         ok = ok && E <= detmath::GPQ_SCALE_HI;
         const double aE = a * E;
         const double pp = prefix * ((B + E) / aE);
@@ -142,28 +123,6 @@ __device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, doubl
         // continued fraction (detmath::gamma_cf_terms; the rescale test folded into the largest |P|)
         double bcf = x + 1.0 - a;
         double Pm = 1.0, Qm = 0.0, P = bcf, Qd = 1.0, di = 0.0, bigP = 0.0;
-#if SHYFT_GSB_U2
-        for (int i = 1; i < 2000; i += 2) {
-            const double d1 = di + 1.0, an1 = -d1 * (d1 - a), b1 = bcf + 2.0;
-            const double P1 = __builtin_fma(b1, P, an1 * Pm), Q1 = __builtin_fma(b1, Qd, an1 * Qm);
-            const double c1 = P1 * Qd, e1 = c1 - P * Q1;
-            const double d2 = d1 + 1.0, an2 = -d2 * (d2 - a), b2 = b1 + 2.0;
-            const double P2 = __builtin_fma(b2, P1, an2 * P), Q2 = __builtin_fma(b2, Q1, an2 * Qd);
-            const double c2 = P2 * Q1, e2 = c2 - P1 * Q2;
-            const bool t1 = __builtin_fabs(e1) <= eps * __builtin_fabs(c1);
-            const bool t2 = __builtin_fabs(e2) <= eps * __builtin_fabs(c2);
-            if (t1 | t2) {
-                if (!t1) bigP = __builtin_fmax(bigP, __builtin_fabs(P1));
-                P = t1 ? P1 : P2;
-                Qd = t1 ? Q1 : Q2;
-                Pm = 0.0;  // (dead)
-                break;
-            }
-            bigP = __builtin_fmax(bigP, __builtin_fmax(__builtin_fabs(P1), __builtin_fabs(P2)));
-            di = d2; bcf = b2; Pm = P1; Qm = Q1; P = P2; Qd = Q2;
-        }
-        if (false)
-#endif
         for (int i = 1; i <= 2000; ++i) {
             di = di + 1.0;
             const double an = -di * (di - a);

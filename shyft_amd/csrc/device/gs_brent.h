@@ -9,10 +9,9 @@
 //  - no calls: exp, log, the series and the continued fraction are inline in the one loop;
 //  - the polynomial constants of exp and log are read once per job from a constant table into SGPRs and used as
 //    SGPR operands of v_fma_f64 (gs_fma_s), instead of two v_mov_b32 per constant per evaluation;
-//  - the series and continued fraction run without their 2^-200 rescale test: with shape a > 0 the series'
-//    E = (a+1)...(a+n) only grows, so a final E <= 2^200/... proves no term rescaled; the fraction's |P| is
-//    checked per term into a flag. A lane whose evaluation would have rescaled, or that leaves the fast domain
-//    (x <= 0, x not normal, a <= 0, |exp argument| > 708), is re-evaluated by the general gs_calc_q.
+//  - the series and continued fraction run without their 2^-200 rescale test (device/gamma_lean.h): a lane whose
+//    evaluation would have rescaled, or that leaves the fast domain (x <= 0, x not normal, a <= 0, |exp argument|
+//    > 708), is re-evaluated by the general gs_calc_q.
 // Bit-identical to gs_corr_lwc (tests: test_ptgsk_parity.py, tools/mb/mb_brent.cpp's device check).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -186,20 +185,6 @@ __device__ __noinline__ double gs_corr_lwc_lean(double z1, double a1, double b1,
 __device__ __noinline__ double gs_corr_lwc_memo(double z1, double a1, double b1, double a2, double b2, double q1,
                                                 double lga2, const gsb_memo& memo) {
     return gs_corr_lwc_lean_t<true>(z1, a1, b1, a2, b2, q1, lga2, &memo);
-}
-
-// the memo of the workgroup-wide speculative opening (kernels/ptgsk.hip): f at the four opening points of the job
-// at fz[0..3] (LDS, written by four lanes of any wavefront before the solve); the points themselves are recomputed
-// here by the same function, so the memo needs no LDS of its own
-__device__ __noinline__ double gs_corr_lwc_memo4(double z1, double a1, double b1, double a2, double b2, double q1,
-                                                 double lga2, const double* fz) {
-    gsb_memo mm;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        mm.z[k] = gs_brent_point(z1, k);
-        mm.f[k] = fz[k];
-    }
-    return gs_corr_lwc_lean_t<true>(z1, a1, b1, a2, b2, q1, lga2, &mm);
 }
 
 }  // namespace shyft_dev

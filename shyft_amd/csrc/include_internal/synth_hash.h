@@ -38,14 +38,24 @@ SYNTH_HD inline double synth_u(uint64_t key, uint64_t var) {
 
 SYNTH_HD inline double synth_elevation(uint64_t seed, uint64_t cell) { return 2000.0 * synth_u(synth_key(seed, cell, 0), 7); }
 
-// v[5] in forcing order: temperature, precipitation, wind_speed, rel_hum, radiation
-SYNTH_HD inline void synth_values(uint64_t seed, uint64_t cell, uint64_t step, double z, double* v) {
+// the cell part of synth_key: synth_key(seed, cell, step) == synth_sm64(synth_cell_key(seed, cell) ^ step)
+SYNTH_HD inline uint64_t synth_cell_key(uint64_t seed, uint64_t cell) {
+    return synth_sm64(seed ^ (cell * 0xD1B54A32D192ED03ull));
+}
+
+// v[5] in forcing order: temperature, precipitation, wind_speed, rel_hum, radiation; ck = synth_cell_key(seed, cell)
+// (hoisted out of a caller's step loop)
+SYNTH_HD inline void synth_values_ck(uint64_t ck, uint64_t step, double z, double* v) {
 #pragma clang fp contract(off)
-    const uint64_t key = synth_key(seed, cell, step);
-    const double f = (double)(step % 8760) / 8760.0;
+    const uint64_t key = synth_sm64(ck ^ step);
+    // step % 8760 and step % 24 in 32-bit arithmetic when the step fits (the same remainders)
+    const bool s32 = (step >> 32) == 0;
+    const uint64_t m8760 = s32 ? (uint64_t)((uint32_t)step % 8760u) : step % 8760;
+    const uint64_t m24 = s32 ? (uint64_t)((uint32_t)step % 24u) : step % 24;
+    const double f = (double)m8760 / 8760.0;
     const double g = f * (1.0 - f);
     const double b = 16.0 * g * g;
-    const double h = (double)(step % 24);
+    const double h = (double)m24;
     const double dd = (h - 12.0) / 6.0;
     double di = 1.0 - dd * dd;
     if (di < 0.0) di = 0.0;
@@ -56,4 +66,8 @@ SYNTH_HD inline void synth_values(uint64_t seed, uint64_t cell, uint64_t step, d
     v[2] = 10.0 * u2;
     v[3] = 0.5 + 0.5 * u3;
     v[4] = 800.0 * di * (0.3 + 0.7 * b);
+}
+
+SYNTH_HD inline void synth_values(uint64_t seed, uint64_t cell, uint64_t step, double z, double* v) {
+    synth_values_ck(synth_cell_key(seed, cell), step, z, v);
 }

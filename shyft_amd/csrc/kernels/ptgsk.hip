@@ -47,15 +47,8 @@ extern "C" int shyft_ptgsk_prof_read(unsigned long long* out) {
 
 namespace {
 
-#ifndef SHYFT_PTGSK_BIG_B
-#define SHYFT_PTGSK_BIG_B 256
-#endif
-constexpr int BLOCK = SHYFT_PTGSK_BIG_B;
-// SPEC4: the speculative Brent opening over the whole workgroup in the large-region instance (4 lanes of any
-// wavefront per job, the f values in jres, the solve itself on the first wavefront)
-#ifndef SHYFT_PTGSK_SPEC4
-#define SHYFT_PTGSK_SPEC4 0
-#endif
+// (128- and 512-lane workgroups measured 7 % and 4 % slower over the year, r05)
+constexpr int BLOCK = 256;
 
 #ifndef SHYFT_LB_WAVES
 #define SHYFT_LB_WAVES 4
@@ -258,21 +251,7 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                 // the speculative opening when the jobs' point lanes fit the solving wavefront: 4 lanes per job
                 // (z1, u1, u2a, u2b: two f rounds saved) or 2 (z1, u1: one round saved)
                 const int L = SPEC ? (4 * nj <= 64 ? 4 : 2 * nj <= 64 ? 2 : 0) : 0;
-                if (!SPEC && SHYFT_PTGSK_SPEC4 && 4 * nj <= B && nj <= 64) {
-                    // every wavefront evaluates opening points (4 lanes per job); f values into jres
-                    const int jj = t >> 2;
-                    if (jj < nj) {
-                        const gsb_zf r = gs_corr_lwc_spec(jz1[jj], ja1[jj], jb1[jj], ja2[jj], jb2[jj], jq1[jj], jlg2[jj], t & 3);
-                        jres[t] = r.f;
-                    }
-                    __syncthreads();
-                    // the solving lanes are all in the first wavefront (nj <= 64): each reads its four memo values
-                    // inside the call, before any of them writes its result over the memo below
-                    if (t < nj) {
-                        const double res = gs_corr_lwc_memo4(jz1[t], ja1[t], jb1[t], ja2[t], jb2[t], jq1[t], jlg2[t], &jres[4 * t]);
-                        jres[t] = res;
-                    }
-                } else if (L) {
+                if (L) {
                     const int jj = L == 4 ? t >> 2 : t >> 1;
                     if (t < 64 && jj < nj) {
                         const gsb_zf r = gs_corr_lwc_spec(jz1[jj], ja1[jj], jb1[jj], ja2[jj], jb2[jj], jq1[jj], jlg2[jj], t & (L - 1));

@@ -23,9 +23,10 @@ __global__ __launch_bounds__(256) void synthetic_forcing_stream_kernel(double* _
          cell += (size_t)gridDim.x * blockDim.x) {
         const double z = zc[cell];
         const uint64_t gcell = cell_offset + (ids ? (uint64_t)ids[cell] : cell);
+        const uint64_t ck = synth_cell_key(seed, gcell);
         for (size_t r = 0; r < n_rows; ++r) {
             double v[5];
-            synth_values(seed, gcell, step0 + r, z, v);
+            synth_values_ck(ck, step0 + r, z, v);
             const size_t o = (row0 + r) * n_cells + cell;
             for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(v[k], &forcing[(size_t)k * win_len * n_cells + o]);
         }
@@ -42,10 +43,11 @@ __global__ __launch_bounds__(256) void synthetic_forcing_kernel(double* __restri
     if (cell >= n_cells) return;
     const double z = zc[cell];
     const uint64_t gcell = cell_offset + (ids ? (uint64_t)ids[cell] : cell);
+    const uint64_t ck = synth_cell_key(seed, gcell);  // once per lane, not per row
     for (size_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
         const uint64_t step = step0 + r;
         double v[5];
-        synth_values(seed, gcell, step, z, v);
+        synth_values_ck(ck, step, z, v);
         const size_t o = (row0 + r) * n_cells + cell;
         for (int k = 0; k < 5; ++k) forcing[(size_t)k * win_len * n_cells + o] = v[k];
     }
