@@ -147,6 +147,11 @@ __device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, doubl
     return r;
 }
 
+// the general evaluation (detmath::gamma_pq with the out-of-line exp / log), out of line
+__device__ __noinline__ gamma_p_result gs_gamma_pq_general(double a, double x, double lga) {
+    return gamma_p_prefix(a, x, lga, detmath::gamma_snow_policy_eps(a));
+}
+
 // gs_gamma_pq (device/special.h) by the lean evaluation, the general one where it does not apply; out of line
 // (one copy, its own register budget)
 __device__ __noinline__ gamma_p_result gs_gamma_pq_lean(double a, double x, double lga) {

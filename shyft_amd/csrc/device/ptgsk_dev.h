@@ -58,8 +58,20 @@ struct gs_lw {
 
 // calc_snow_state's incomplete gamma: the lean out-of-line evaluation (device/gamma_lean.h; the general one where it
 // does not apply). 1M cells, the year in 730-step chunks: 92.7 -> 91.6 ms per chunk, bit-exact (r05 variants)
+#ifndef SHYFT_CS_INL
+#define SHYFT_CS_INL 0
+#endif
 __device__ __forceinline__ gamma_p_result gs_gamma_pq_cs(double a, double x, double lga) {
+#if SHYFT_CS_INL
+    // (variant builds) the lean evaluation inline, the general one out of line for the lanes it does not cover
+    const gsb_k k = gsb_load();
+    bool ok;
+    gamma_p_result r = gsb_gamma_pq(a, x, lga, detmath::gamma_snow_policy_eps(a), a + 1.0, k, ok);
+    if (!ok) r = gs_gamma_pq_general(a, x, lga);
+    return r;
+#else
     return gs_gamma_pq_lean(a, x, lga);
+#endif
 }
 
 // gamma_snow.h:230-260
