@@ -8,9 +8,12 @@
 
 namespace shyft_dev {
 
-// Priestley-Taylor's exp / log inline by the gamma_lean.h fast paths (SGPR constant table), the out-of-line general
-// function only beyond them -- the same bits as dexp / dlog. Measured (r05, year mean per 730-step chunk):
-// hbv_stack 512K cells 7.6 -> 7.5 ms, pt_gs_k 1M cells 91.7 -> 90.8 ms, bit-exact
+// exp / log by the gamma_lean.h fast paths inline (SGPR constant table), the out-of-line general function only
+// beyond them -- the same bits as dexp / dlog. Whether inline or out-of-line calls are faster depends on the kernel's
+// register pressure, so the callers choose (template argument INL): measured (r05, same box, year means per
+// 730-step chunk) pt_gs_k 92.1 -> 90.0 ms with PT and Kirchner inline, but hbv_stack 7.7 -> 8.0 ms and pt_hs_k
+// 34.3 -> 37.9 ms, pt_ss_k unchanged -- so only pt_gs_k takes them inline.
+// mathematics of a kernel: out-of-line calls (INL = false) or inline fast paths (INL = true)
 __device__ __forceinline__ double exp_fast(double x, const gsb_k& k) {
     double r = gsb_exp(x, k);
     if (!(__builtin_fabs(x) <= 708.0)) r = dexp(x);
@@ -22,19 +25,41 @@ __device__ __forceinline__ double log_fast(double x, const gsb_k& k) {
     return r;
 }
 
+template <bool INL>
+struct kmath {
+    __device__ kmath() {}
+    __device__ double exp(double x) const { return dexp(x); }
+    __device__ double log(double x) const { return dlog(x); }
+    __device__ dexp_pair exp2(double x, double y) const { return dexp2(x, y); }
+};
+template <>
+struct kmath<true> {
+    gsb_k k;
+    __device__ kmath() : k(gsb_load()) {}
+    __device__ double exp(double x) const { return exp_fast(x, k); }
+    __device__ double log(double x) const { return log_fast(x, k); }
+    __device__ dexp_pair exp2(double x, double y) const {
+        dexp_pair r;
+        r.a = exp_fast(x, k);
+        r.b = exp_fast(y, k);
+        return r;
+    }
+};
+
 // returns potential evapotranspiration in mm/s (priestley_taylor.h:75-102)
+template <bool INL = false>
 __device__ inline double pt_pot_evap(double albedo, double alpha, double temperature, double global_radiation,
                                      double rhumidity) {
     const bool neg = temperature < 0;
     const double ck2 = neg ? 17.84362 : 17.08085;
     const double ck3 = neg ? 245.425 : 234.175;
     const double ctt_inv = 1 / (ck3 + temperature);
-    const gsb_k k = gsb_load();
-    const double sat_pressure = 0.610780 * exp_fast(ck2 * temperature * ctt_inv, k);
+    const kmath<INL> km;
+    const double sat_pressure = 0.610780 * km.exp(ck2 * temperature * ctt_inv);
     const double delta = sat_pressure * ck2 * ck3 * ctt_inv * ctt_inv;
     const double vapour_pressure = sat_pressure * rhumidity;
     const double k_temp = temperature + 273.15;
-    const double e_atm = 1.24 * exp_fast(0.143 * log_fast(10 * vapour_pressure / k_temp, k), k) * (0.85 + 0.5 * rhumidity);
+    const double e_atm = 1.24 * km.exp(0.143 * km.log(10 * vapour_pressure / k_temp)) * (0.85 + 0.5 * rhumidity);
     const double net_rad = 0.0000000567 * dpow4(k_temp) * (e_atm - 0.98) + global_radiation * (1.0 - albedo);
     const double epot = alpha * delta * net_rad / (delta + 0.066);
     if (epot < 0.0) return 0.0;
@@ -43,19 +68,21 @@ __device__ inline double pt_pot_evap(double albedo, double alpha, double tempera
 
 // the same, plus exp(ae_arg) for the caller's actual_evapotranspiration (inline beside the saturation
 // pressure's exp (two independent exps side by side instead of back to back); the same bits as the two calls
+template <bool INL = false>
 __device__ inline double pt_pot_evap_exp(double albedo, double alpha, double temperature, double global_radiation,
                                          double rhumidity, double ae_arg, double& ae_exp) {
     const bool neg = temperature < 0;
     const double ck2 = neg ? 17.84362 : 17.08085;
     const double ck3 = neg ? 245.425 : 234.175;
     const double ctt_inv = 1 / (ck3 + temperature);
-    const gsb_k k = gsb_load();
-    const double sat_pressure = 0.610780 * exp_fast(ck2 * temperature * ctt_inv, k);
-    ae_exp = exp_fast(ae_arg, k);
+    const kmath<INL> km;
+    const dexp_pair e2 = km.exp2(ck2 * temperature * ctt_inv, ae_arg);
+    ae_exp = e2.b;
+    const double sat_pressure = 0.610780 * e2.a;
     const double delta = sat_pressure * ck2 * ck3 * ctt_inv * ctt_inv;
     const double vapour_pressure = sat_pressure * rhumidity;
     const double k_temp = temperature + 273.15;
-    const double e_atm = 1.24 * exp_fast(0.143 * log_fast(10 * vapour_pressure / k_temp, k), k) * (0.85 + 0.5 * rhumidity);
+    const double e_atm = 1.24 * km.exp(0.143 * km.log(10 * vapour_pressure / k_temp)) * (0.85 + 0.5 * rhumidity);
     const double net_rad = 0.0000000567 * dpow4(k_temp) * (e_atm - 0.98) + global_radiation * (1.0 - albedo);
     const double epot = alpha * delta * net_rad / (delta + 0.066);
     if (epot < 0.0) return 0.0;

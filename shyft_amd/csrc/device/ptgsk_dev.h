@@ -212,11 +212,14 @@ struct gs_cell {
 // P is the per-set parameter row (layout.h); dt_s = to_seconds(dt), dt_us the
 // microsecond count (prec = prec_mm_h*dt/HOUR, outflow*HOUR/dt as the reference
 // evaluates them).
+// gs_front writes the state fields it has finished (albedo, surface_heat, iso_pot_energy, and alpha,
+// sdc_melt_mean, acc_melt as gs_back starts from them) straight into the state; gs_mid carries only what gs_back
+// needs besides the state, so fewer values stay live across the workgroup's Brent phase (r05: 16 -> 6 doubles;
+// the same values in the same operations)
 struct gs_mid {
     bool done;  // the early "no snow" path was taken (gamma_snow.h:313-322)
     bool need;  // a corr_lwc job was handed to the caller's enqueue
-    double prec, snow, rain, albedo, lwc, surface_heat, alpha, temp_swe, sca, storage, sdc_melt_mean, acc_melt,
-        iso_pot_energy, potential_melt, start_storage, sdc_scale;
+    double snow, rain, storage, potential_melt, start_storage, sdc_scale;
 };
 
 // The snow storage of the state as it leaves a step: gs_back's final calc_snow_state(alpha, sdc_melt_mean/alpha,
@@ -234,7 +237,7 @@ struct gs_carry {
 // or NaN, lga2 = lgamma(a2)): the kernel writes it straight into its workgroup's LDS job queue, so the seven job
 // values are not held in registers (or scratch) until a later queue pass
 template <class LGC, class Enqueue>
-__device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
+__device__ inline void gs_front(gs_state& s, gs_mid& m, bool start_melt, double dt_s, double dt_us,
                                       const double* __restrict__ P, const gs_cell& cc, double T, double rad,
                                       double prec_mm_h, double wind_speed, double rel_hum, LGC& lgc,
                                       const gs_carry& carry, Enqueue&& enqueue) {
@@ -248,10 +251,8 @@ __device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, d
     double snow, rain;
     if (T < P[PK_TX]) { snow = prec; rain = 0.0; }
     else { snow = 0.0; rain = prec; }
-    m.prec = prec;
-    m.acc_melt = acc_melt;
     if (snow < GS_TOL && sdc_melt_mean < GS_TOL && acc_melt < 0.0) {
-        m.done = true;
+        m.done = true;  // (acc_melt was not reset here: the early path needs acc_melt < 0)
         return;
     }
     double albedo = s.albedo;
@@ -338,19 +339,19 @@ __device__ inline void gs_front(const gs_state& s, gs_mid& m, bool start_melt, d
             }
         }
     }
+    (void)sca;  // (its value is dead: gs_back's final calc_snow_state assigns sca)
     m.snow = snow;
     m.rain = rain;
-    m.albedo = albedo;
-    m.lwc = lwc;
-    m.surface_heat = surface_heat;
-    m.alpha = alpha;
-    m.temp_swe = temp_swe;
-    m.sca = sca;
     m.storage = storage;
-    m.sdc_melt_mean = sdc_melt_mean;
-    m.iso_pot_energy = iso_pot_energy;
     m.potential_melt = potential_melt;
     m.sdc_scale = sdc_scale;
+    s.albedo = albedo;
+    s.surface_heat = surface_heat;
+    s.iso_pot_energy = iso_pot_energy;
+    s.alpha = alpha;
+    s.sdc_melt_mean = sdc_melt_mean;
+    s.acc_melt = acc_melt;
+    // (lwc and temp_swe are unchanged until gs_back)
 }
 
 template <class LGC>
@@ -362,7 +363,7 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
         s.albedo = P[PK_MAX_ALBEDO];
         s.surface_heat = 0.0;
         s.iso_pot_energy = 0.0;
-        s.acc_melt = m.acc_melt;  // == s.acc_melt: the early path only triggers when it was not reset
+        // (s.acc_melt as it was: the early path only triggers when it was not reset)
         r_sca = 0.0;
         r_storage = 0.0;
         r_outflow = prec_mm_h;
@@ -370,10 +371,11 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
     }
     const double ibgf = P[PK_IBGF];
     const double max_water = P[PK_MAX_WATER];
+    const double prec = (prec_mm_h * dt_us) / 3600000000.0;  // gs_front's expression
     double snow = m.snow;
     const double rain = m.rain;
-    double lwc = m.lwc, alpha = m.alpha, temp_swe = m.temp_swe, sca = m.sca, storage = m.storage;
-    double sdc_melt_mean = m.sdc_melt_mean, acc_melt = m.acc_melt, potential_melt = m.potential_melt;
+    double lwc = s.lwc, alpha = s.alpha, temp_swe = s.temp_swe, sca = 0.0, storage = m.storage;
+    double sdc_melt_mean = s.sdc_melt_mean, acc_melt = s.acc_melt, potential_melt = m.potential_melt;
     double sdc_scale = m.sdc_scale;
     if (acc_melt < 0.0) {
         // the reference follows corr_lwc with calc_snow_state(alpha, sdc_scale, ..., lwc, ..., storage, sca)
@@ -429,16 +431,13 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
     calc_snow_state(alpha, sdc_scale, ibgf, acc_melt, lwc, max_water, temp_swe, storage, sca, lgc, carry.lw);
     carry.storage = storage;
     carry.ok = true;
-    double outflow = m.prec + m.start_storage - storage;
+    double outflow = prec + m.start_storage - storage;
     if (outflow < 0.0) outflow = 0.0;
 
-    s.albedo = m.albedo;
     s.lwc = lwc;
-    s.surface_heat = m.surface_heat;
     s.alpha = alpha;
     s.sdc_melt_mean = sdc_melt_mean;
     s.acc_melt = acc_melt;
-    s.iso_pot_energy = m.iso_pot_energy;
     s.temp_swe = temp_swe;
     r_sca = sca;
     r_storage = storage;
@@ -459,9 +458,10 @@ __device__ inline double kirchner_f(double ln_q, double p_minus_e, double c1, do
 // accepted) is flattened into one loop of try_steps so lanes of a wave that
 // need different numbers of attempts stay in one convergent loop.
 // Returns false if a do_step needed 500 attempts (odeint failed_step_checker).
-// The step's exps and logs run inline by the gamma_lean.h fast paths (one SGPR constant table per call, the general
-// out-of-line functions only beyond them) instead of out-of-line dexp2 / dexp / dlog calls -- the same bits.
-// 1M cells, the year in 730-step chunks: 90.8 -> 89.7 ms per chunk (r05 variants).
+// INL: the step's exps and logs inline by the gamma_lean.h fast paths (one SGPR constant table per call, the general
+// out-of-line functions only beyond them) instead of out-of-line dexp2 / dexp / dlog calls -- the same bits (pt_gs_k:
+// 90.8 -> 89.7 ms per 730-step chunk; the other stacks keep the calls, device/pt_dev.h)
+template <bool INL = false>
 __device__ inline bool kirchner_step(double& q, double& q_avg, double p, double e, double t1, double c1, double c2,
                                      double c3) {
     const double abs_err = 1.0e-7, rel_err = 1.0e-8;
@@ -470,13 +470,13 @@ __device__ inline bool kirchner_step(double& q, double& q_avg, double p, double 
     q_avg = q; q = q + 0.01 * (p - e); return true;  // timing ablation only (wrong results)
 #endif
     const double pe = p - e;
-    const gsb_k kk = gsb_load();
+    const kmath<INL> km;
     auto kirchner_f = [&](double ln_q, double p_minus_e, double c1_, double c2_, double c3_) {
-        const double ga = exp_fast(c1_ + c2_ * ln_q + c3_ * ln_q * ln_q, kk), gb = exp_fast(-ln_q, kk);
-        return ga >= 1.e-30 ? ga * (p_minus_e * gb - 1.0) : 0.0;
+        const dexp_pair ge = km.exp2(c1_ + c2_ * ln_q + c3_ * ln_q * ln_q, -ln_q);
+        return ge.a >= 1.e-30 ? ge.a * (p_minus_e * ge.b - 1.0) : 0.0;
     };
-    auto dexp = [&](double v) { return exp_fast(v, kk); };
-    auto dlog = [&](double v) { return log_fast(v, kk); };
+    auto dexp = [&](double v) { return km.exp(v); };
+    auto dlog = [&](double v) { return km.log(v); };
     double x = dlog(q);
     double dxdt = kirchner_f(x, pe, c1, c2, c3);
     double t = 0.0, dt = t1;

@@ -301,12 +301,13 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         // Priestley-Taylor's saturation-pressure exp and actual_evapotranspiration's exp in one dexp2 call
         double ae_exp;
         const double pot_evap =
-            pt_pot_evap_exp(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum, -q * 3.0 / P[PK_AE_SCALE], ae_exp) * 3600.0;
+            pt_pot_evap_exp<true>(P[PK_PT_ALBEDO], P[PK_PT_ALPHA], temp, rad, rel_hum, -q * 3.0 / P[PK_AE_SCALE], ae_exp) *
+            3600.0;
         const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(gs_sca, glacier_fraction));
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         PROF_MARK(4);  // glacier, PT, AE
         double q_avg;
-        if (!kirchner_step(q, q_avg, gs_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
+        if (!kirchner_step<true>(q, q_avg, gs_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
                            ae, a.t1_hours, kc1, kc2, kc3))
             err = ERR_KIRCHNER_MAX_ITER;
         const double total_discharge = smax(0.0, prec - ae) * direct_response_fraction + gm_direct * gm_mmh +
@@ -375,8 +376,8 @@ __global__ __launch_bounds__(256, 8) void ptgsk_callee_budget_kernel(const ptgsk
     const double z = gs_corr_lwc_lean(j[0], j[1], j[2], j[3], j[4], j[5], j[6]);
     gs_back(s, m, z, sca, sto, outf, c == 1, a.dt_us, a.params, gc, q, lgc, carry);
     double e;
-    const double pe = pt_pot_evap_exp(0.2, 1.26, q, q, q, q, e);
-    kirchner_step(q, qa, outf, pe * e, a.t1_hours, -2.4, 0.9, -0.1);
+    const double pe = pt_pot_evap_exp<true>(0.2, 1.26, q, q, q, q, e);
+    kirchner_step<true>(q, qa, outf, pe * e, a.t1_hours, -2.4, 0.9, -0.1);
     a.resp[c] = q + qa + sca + sto + s.lwc;
 }
 

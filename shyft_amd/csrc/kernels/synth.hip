@@ -49,7 +49,9 @@ __global__ __launch_bounds__(256) void synthetic_forcing_kernel(double* __restri
         double v[5];
         synth_values_ck(ck, step, z, v);
         const size_t o = (row0 + r) * n_cells + cell;
-        for (int k = 0; k < 5; ++k) forcing[(size_t)k * win_len * n_cells + o] = v[k];
+        // streaming stores: a window (17.5 GB at 1M cells x 438 steps) is far larger than L2 / MALL
+        // (59.4 -> 59.2 ms per bench step, r05)
+        for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(v[k], &forcing[(size_t)k * win_len * n_cells + o]);
     }
 }
 
