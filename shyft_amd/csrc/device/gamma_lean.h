@@ -7,7 +7,8 @@
 //    E = (a+1)...(a+n) only grows, so a final E <= 2^200/... proves no term rescaled; the fraction's largest |P| is
 //    kept with a max (no per-term branch) and checked after the loop. An evaluation that would have rescaled, or
 //    that leaves the fast domain, is redone by the general detmath evaluation.
-// Used by the Brent job of device/gs_brent.h (its f) and by calc_snow_state (device/ptgsk_dev.h).
+// Used by the Brent job of device/gs_brent.h (its f), by calc_snow_state (device/ptgsk_dev.h) and by Skaugen's
+// sca_rel_red (device/ptssk_dev.h); exp_fast / log_fast are the kernels' inline exp / log (device/pt_dev.h kmath).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -91,6 +92,18 @@ __device__ __forceinline__ double gsb_log(double x, const gsb_k& k) {
     return sum + small;
 }
 
+// dexp / dlog bit for bit: the fast paths above inline, the out-of-line general function beyond them
+__device__ __forceinline__ double exp_fast(double x, const gsb_k& k) {
+    double r = gsb_exp(x, k);
+    if (!(__builtin_fabs(x) <= 708.0)) r = dexp(x);
+    return r;
+}
+__device__ __forceinline__ double log_fast(double x, const gsb_k& k) {
+    double r = gsb_log(x, k);
+    if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) r = dlog(x);
+    return r;
+}
+
 // P(a, x), P(a+1, x) and the prefix by detmath::gamma_pq's series / continued fraction for the fast domain;
 // ok = false: the caller takes the general evaluation (the value returned is then meaningless)
 __device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, double lga, double eps, double ap1,
@@ -150,17 +163,6 @@ __device__ __forceinline__ gamma_p_result gsb_gamma_pq(double a, double x, doubl
 // the general evaluation (detmath::gamma_pq with the out-of-line exp / log), out of line
 __device__ __noinline__ gamma_p_result gs_gamma_pq_general(double a, double x, double lga) {
     return gamma_p_prefix(a, x, lga, detmath::gamma_snow_policy_eps(a));
-}
-
-// gs_gamma_pq (device/special.h) by the lean evaluation, the general one where it does not apply; out of line
-// (one copy, its own register budget)
-__device__ __noinline__ gamma_p_result gs_gamma_pq_lean(double a, double x, double lga) {
-    const gsb_k k = gsb_load();
-    const double eps = detmath::gamma_snow_policy_eps(a);
-    bool ok;
-    const gamma_p_result r = gsb_gamma_pq(a, x, lga, eps, a + 1.0, k, ok);
-    if (ok) return r;
-    return gamma_p_prefix(a, x, lga, eps);
 }
 
 }  // namespace shyft_dev

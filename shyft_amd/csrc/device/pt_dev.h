@@ -13,18 +13,7 @@ namespace shyft_dev {
 // register pressure, so the callers choose (template argument INL): measured (r05, same box, year means per
 // 730-step chunk) pt_gs_k 92.1 -> 90.0 ms with PT and Kirchner inline, but hbv_stack 7.7 -> 8.0 ms and pt_hs_k
 // 34.3 -> 37.9 ms, pt_ss_k unchanged -- so only pt_gs_k takes them inline.
-// mathematics of a kernel: out-of-line calls (INL = false) or inline fast paths (INL = true)
-__device__ __forceinline__ double exp_fast(double x, const gsb_k& k) {
-    double r = gsb_exp(x, k);
-    if (!(__builtin_fabs(x) <= 708.0)) r = dexp(x);
-    return r;
-}
-__device__ __forceinline__ double log_fast(double x, const gsb_k& k) {
-    double r = gsb_log(x, k);
-    if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) r = dlog(x);
-    return r;
-}
-
+// mathematics of a kernel: out-of-line calls (INL = false) or inline fast paths (INL = true: exp_fast / log_fast)
 template <bool INL>
 struct kmath {
     __device__ kmath() {}

@@ -56,22 +56,15 @@ struct gs_lw {
     double p = __builtin_nan(""), p1 = __builtin_nan("");
 };
 
-// calc_snow_state's incomplete gamma: the lean out-of-line evaluation (device/gamma_lean.h; the general one where it
-// does not apply). 1M cells, the year in 730-step chunks: 92.7 -> 91.6 ms per chunk, bit-exact (r05 variants)
-#ifndef SHYFT_CS_INL
-#define SHYFT_CS_INL 0
-#endif
+// calc_snow_state's incomplete gamma: the lean evaluation (device/gamma_lean.h) inline, the general one out of line
+// for the lanes it does not cover. 1M cells, the year in 730-step chunks (r05 variants, bit-exact): 92.7 -> 91.6 ms
+// per chunk out of line, 85.2 -> 84.0 inline (after the gs_mid slimming)
 __device__ __forceinline__ gamma_p_result gs_gamma_pq_cs(double a, double x, double lga) {
-#if SHYFT_CS_INL
-    // (variant builds) the lean evaluation inline, the general one out of line for the lanes it does not cover
     const gsb_k k = gsb_load();
     bool ok;
     gamma_p_result r = gsb_gamma_pq(a, x, lga, detmath::gamma_snow_policy_eps(a), a + 1.0, k, ok);
     if (!ok) r = gs_gamma_pq_general(a, x, lga);
     return r;
-#else
-    return gs_gamma_pq_lean(a, x, lga);
-#endif
 }
 
 // gamma_snow.h:230-260
@@ -214,12 +207,13 @@ struct gs_cell {
 // evaluates them).
 // gs_front writes the state fields it has finished (albedo, surface_heat, iso_pot_energy, and alpha,
 // sdc_melt_mean, acc_melt as gs_back starts from them) straight into the state; gs_mid carries only what gs_back
-// needs besides the state, so fewer values stay live across the workgroup's Brent phase (r05: 16 -> 6 doubles;
-// the same values in the same operations)
+// needs besides the state, so fewer values stay live across the workgroup's Brent phase (r05: 16 -> 5 doubles;
+// the same values in the same operations; 1M cells, 730-step chunks: 92.0 -> 85.0 ms per chunk). Recomputing
+// snow / rain / sdc_scale in gs_back instead of carrying them measured no better.
 struct gs_mid {
     bool done;  // the early "no snow" path was taken (gamma_snow.h:313-322)
     bool need;  // a corr_lwc job was handed to the caller's enqueue
-    double snow, rain, storage, potential_melt, start_storage, sdc_scale;
+    double snow, rain, potential_melt, start_storage, sdc_scale;  // (gs_front leaves storage == start_storage)
 };
 
 // The snow storage of the state as it leaves a step: gs_back's final calc_snow_state(alpha, sdc_melt_mean/alpha,
@@ -342,7 +336,6 @@ __device__ inline void gs_front(gs_state& s, gs_mid& m, bool start_melt, double 
     (void)sca;  // (its value is dead: gs_back's final calc_snow_state assigns sca)
     m.snow = snow;
     m.rain = rain;
-    m.storage = storage;
     m.potential_melt = potential_melt;
     m.sdc_scale = sdc_scale;
     s.albedo = albedo;
@@ -360,6 +353,8 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
                                      const gs_cell& cc, double prec_mm_h, LGC& lgc, gs_carry& carry) {
     if (m.done) {
         carry.ok = false;
+        carry.storage = 0.0;  // (never read while ok is false: defined here so that the carry is dead across the
+        carry.lw = gs_lw();   // workgroup's Brent phase; r05: VGPR spills 49 -> 26, 83.4 -> 82.9 ms per chunk)
         s.albedo = P[PK_MAX_ALBEDO];
         s.surface_heat = 0.0;
         s.iso_pot_energy = 0.0;
@@ -374,7 +369,8 @@ __device__ inline void gs_back(gs_state& s, const gs_mid& m, double z, double& r
     const double prec = (prec_mm_h * dt_us) / 3600000000.0;  // gs_front's expression
     double snow = m.snow;
     const double rain = m.rain;
-    double lwc = s.lwc, alpha = s.alpha, temp_swe = s.temp_swe, sca = 0.0, storage = m.storage;
+    double lwc = s.lwc, alpha = s.alpha, temp_swe = s.temp_swe, sca = 0.0;
+    double storage = m.start_storage;
     double sdc_melt_mean = s.sdc_melt_mean, acc_melt = s.acc_melt, potential_melt = m.potential_melt;
     double sdc_scale = m.sdc_scale;
     if (acc_melt < 0.0) {

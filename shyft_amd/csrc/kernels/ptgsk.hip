@@ -20,6 +20,7 @@
 
 #include "../device/ptgsk_dev.h"
 #include "../device/gs_brent.h"
+#include "../device/wave_place.h"
 #include "../include_internal/kernels.h"
 
 using namespace shyft_dev;
@@ -161,10 +162,14 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     __shared__ double jz1[B], ja1[B], jb1[B], ja2[B], jb2[B], jq1[B], jlg2[B], jres[B];
     __shared__ double jsz[SPEC ? 64 : 1], jsf[SPEC ? 64 : 1];  // speculative opening: point and f of lane t
     __shared__ int jcount[2];
+    __shared__ int wsimd[B / 64];
+    publish_wave_simd(wsimd);
     if (COMPACT) {
         if (threadIdx.x == 0) jcount[0] = jcount[1] = 0;  // both: the first step may be odd (start_step)
         __syncthreads();
     }
+    // the lane that solves job 0: the first lane of the solving wavefront (device/wave_place.h)
+    const int jrot = solver_lane0<B>(wsimd);
 
     auto collect_state = [&](size_t wi) {
         // state_collector::collect of state.scale_snow(snow_storage_fraction)
@@ -228,23 +233,13 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
             if (nj > 0) {
 #ifdef SHYFT_PROF
                 const unsigned long long tb = __builtin_amdgcn_s_memtime();
-                int nf = 0;
-                for (int j = threadIdx.x; j < nj; j += B) jres[j] = gs_corr_lwc(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j], nf);
-                if (threadIdx.x < nj) {  // solver lanes: wave sum and wave max of f evaluations
-                    int sum = nf, mx = nf;
-                    for (int o = 32; o > 0; o >>= 1) {
-                        sum += __shfl_xor(sum, o, 64);
-                        const int m2 = __shfl_xor(mx, o, 64);
-                        mx = m2 > mx ? m2 : mx;
-                    }
-                    if ((threadIdx.x & 63) == 0) {
-                        atomicAdd(&g_ptgsk_prof[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb));
-                        atomicAdd(&g_ptgsk_prof[9], (unsigned long long)mx);
-                        atomicAdd(&g_ptgsk_prof[10], (unsigned long long)sum);
-                    }
-                }
+                if (threadIdx.x < nj) __builtin_amdgcn_s_setprio(BRENT_PRIO);
+                for (int j = threadIdx.x; j < nj; j += B) jres[j] = GS_BRENT_JOB(jz1[j], ja1[j], jb1[j], ja2[j], jb2[j], jq1[j], jlg2[j]);
+                __builtin_amdgcn_s_setprio(0);
+                if (threadIdx.x < nj && (threadIdx.x & 63) == 0)
+                    atomicAdd(&g_ptgsk_prof[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - tb));
 #else
-                const int t = threadIdx.x;
+                const int t = SPEC ? (int)threadIdx.x : (int)((threadIdx.x - jrot) & (B - 1));
                 // the solving wavefront is the workgroup's critical path (its other wavefronts wait at the
                 // barrier below): it gets issue priority over the other workgroups' wavefronts on its SIMD
                 if (t < nj) __builtin_amdgcn_s_setprio(BRENT_PRIO);
@@ -283,7 +278,10 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
             }
         }
         PROF_MARK(2);  // Brent phase
-        if (!valid) continue;
+        if (!valid) {
+            carry = gs_carry();  // (dead: keeps the carry out of the values live across the Brent phase)
+            continue;
+        }
         double gs_sca, gs_storage, gs_outflow;
         LOAD_GCELL();
 #ifdef SHYFT_ABLATE_SNOW  // instruction-budget ablation only (wrong results): no snow routine at all

@@ -15,6 +15,7 @@
 #include "../device/pt_dev.h"
 #include "../device/ptgsk_dev.h"
 #include "../device/ptssk_dev.h"
+#include "../device/wave_place.h"
 #include "../include_internal/kernels.h"
 
 using namespace shyft_dev;
@@ -136,6 +137,12 @@ void ptssk_run_kernel(const ptssk_kargs a) {
         SS[SSC_RESIDUAL * SSS + o] = s.residual;
     };
 
+    // the lane that solves job 0: the first lane of the solving wavefront (device/wave_place.h)
+    __shared__ int wsimd[BLOCK / 64];
+    publish_wave_simd(wsimd);
+    __syncthreads();
+    const int jrot = solver_lane0<BLOCK>(wsimd);
+
     const int i_end = a.step0 + a.n_steps;
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
@@ -161,8 +168,9 @@ void ptssk_run_kernel(const ptssk_kargs a) {
             __syncthreads();
             const int nj = jcount[i & 1];
             if (nj > 0) {
-                if ((int)threadIdx.x < nj) __builtin_amdgcn_s_setprio(JOB_PRIO);  // the workgroup's critical path
-                for (int j = threadIdx.x; j < nj; j += BLOCK) {
+                const int t = (int)((threadIdx.x - jrot) & (BLOCK - 1));
+                if (t < nj) __builtin_amdgcn_s_setprio(JOB_PRIO);  // the workgroup's critical path
+                for (int j = t; j < nj; j += BLOCK) {
                     int32_t e = 0;
                     jres[j] = ss_sca_rel_red(ju[j], jn[j], jnu[j], jal[j], e);
                     jerr[j] = e;
