@@ -1,12 +1,14 @@
 // Which wavefront of a workgroup solves the workgroup's job queue (pt_gs_k Brent jobs, pt_ss_k sca_rel_red jobs).
 //
 // While one wavefront solves, the workgroup's other wavefronts wait at a barrier, so the solving wavefronts of the
-// workgroups resident on a CU are the CU's busy ones. With the first wavefront as the solver they all sat on the
-// same SIMD (wave 0 of every workgroup, as the measurement below suggests), one SIMD issuing for four solvers while three idled. Each wavefront reads
-// its SIMD from the HW_ID hardware register (s_getreg, a register read), the workgroup publishes the four in LDS,
-// and the solver is the wavefront on SIMD (HW_ID.TG_ID & 3): TG_ID is the workgroup's id on its CU, so co-resident
-// workgroups mostly solve on different SIMDs. Which wavefront solves changes no result (the same jobs, the
-// same function); if no wavefront of the workgroup is on that SIMD the first one solves.
+// workgroups resident on a CU are the CU's busy ones, and two of them on one SIMD share its issue slots while
+// another SIMD idles. Wave 0's SIMD follows the dispatcher's rotation, which puts some co-resident workgroups' wave 0
+// on the same SIMD (tools/mb/probe_hwid: 280 of 6,677 overlapping pairs of 256-lane workgroups). Here each
+// wavefront reads its SIMD from the HW_ID hardware register (s_getreg, a register read), the workgroup publishes
+// the four in LDS, and the solver is the wavefront on SIMD (HW_ID.TG_ID & 3): TG_ID is the workgroup's slot on its
+// CU (0-3 with 4 resident), so co-resident workgroups solve on different SIMDs (probe: 0 of 6,677 pairs share one).
+// Which wavefront solves changes no result (the same jobs, the same function); if no wavefront of the workgroup is
+// on that SIMD the first one solves.
 // Measured r05 (1M cells, 730-step chunks, year mean): pt_gs_k 82.7 -> 80.6 ms (January 131 -> 125, October
 // 143 -> 134); rotating by block index instead (blockIdx & 3, blockIdx >> 3 & 3) changed nothing.
 #pragma once
