@@ -16,83 +16,7 @@
 
 namespace shyft_dev {
 
-// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: 2/25 .. 2/3, LN2_HI LN2_LO
-static __constant__ double gsb_const[32] = {
-    1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
-    1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
-    2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04, 1.3888888888888889e-03,
-    8.3333333333333333e-03, 4.1666666666666664e-02, 1.6666666666666666e-01,
-    2.0 / 25, 2.0 / 23, 2.0 / 21, 2.0 / 19, 2.0 / 17, 2.0 / 15, 2.0 / 13, 2.0 / 11, 2.0 / 9, 2.0 / 7, 2.0 / 5,
-    2.0 / 3, 0.0, 0.0, 0.0, 0.0, 0.0};
-
-typedef __attribute__((address_space(4))) const double gsb_cdouble;
-
-// a * b + c with c an SGPR pair (wave-uniform constant): one v_fma_f64, no v_mov of the constant
-__device__ __forceinline__ double gs_fma_s(double a, double b, double c) {
-    double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
-    return d;
-}
-
-struct gsb_k {
-    double c[27];
-};
-
-__device__ __forceinline__ gsb_k gsb_load() {
-    gsb_k k;
-    const gsb_cdouble* __restrict__ p = (const gsb_cdouble*)gsb_const;
-    asm volatile("" : "+s"(p));  // keep the table opaque: scalar loads into SGPRs, not folded literals
-#pragma unroll
-    for (int i = 0; i < 27; ++i) k.c[i] = p[i];
-    return k;
-}
-
-// detmath::exp for |x| <= 708 (exp_poly + one ldexp)
-__device__ __forceinline__ double gsb_exp(double x, const gsb_k& k) {
-    const double t = x * k.c[0] + k.c[1];
-    const double kf = t - k.c[1];
-    double r = __builtin_fma(-kf, k.c[2], x);
-    r = __builtin_fma(-kf, k.c[3], r);
-    double p = gs_fma_s(r, k.c[4], k.c[5]);
-#pragma unroll
-    for (int i = 6; i <= 14; ++i) p = gs_fma_s(p, r, k.c[i]);
-    p = __builtin_fma(p, r, 0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
-    return __builtin_ldexp(p, (int)kf);
-}
-
-// detmath::log for positive normal finite x (log_dd without its subnormal branch, hi part)
-__device__ __forceinline__ double gsb_log(double x, const gsb_k& k) {
-    const uint64_t u = (uint64_t)__double_as_longlong(x);
-    int e = (int)((u >> 52) & 0x7ff) - 1023;
-    double m = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
-    if (m > 1.4142135623730951) {
-        m = m * 0.5;
-        e += 1;
-    }
-    const double f = m - 1.0;
-    const double d = 2.0 + f;
-    const double d_lo = (2.0 - d) + f;
-    const double s = f / d;
-    const double s_lo = (__builtin_fma(-s, d, f) - s * d_lo) / d;
-    const double z = s * s;
-    double t = gs_fma_s(k.c[15], z, k.c[16]);
-#pragma unroll
-    for (int i = 17; i <= 26; ++i) t = gs_fma_s(t, z, k.c[i]);
-    const double tail = (s * z) * t;
-    const double ed = (double)e;
-    const double a_hi = ed * k.c[2];
-    const double a_lo = ed * k.c[3];
-    const double b = 2.0 * s;
-    const double sum = a_hi + b;
-    const double bb = sum - a_hi;
-    const double err = (a_hi - (sum - bb)) + (b - bb);
-    const double small = ((err + 2.0 * s_lo) + tail) + a_lo;
-    return sum + small;
-}
-
-// dexp / dlog bit for bit: the fast paths above inline, the out-of-line general function beyond them
+// dexp / dlog bit for bit: the fast paths of device/fastmath.h inline, the out-of-line general function beyond them
 __device__ __forceinline__ double exp_fast(double x, const gsb_k& k) {
     double r = gsb_exp(x, k);
     if (!(__builtin_fabs(x) <= 708.0)) r = dexp(x);

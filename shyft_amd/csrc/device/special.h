@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../../detmath/detmath.h"
+#include "fastmath.h"
 
 namespace shyft_dev {
 
@@ -23,8 +24,24 @@ __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b 
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
 // the elementary functions are out-of-line device functions (one copy each: I-cache and register pressure of the
 // step loops), the physics around them is inlined
+#ifndef SHYFT_TABLE_CALLS
+#define SHYFT_TABLE_CALLS 0
+#endif
+#if SHYFT_TABLE_CALLS
+// (per kernel file) the fast paths with SGPR-table constants (device/fastmath.h): fewer VALU instructions per call
+// (no v_mov_b32 pair per constant), more SGPRs clobbered across it; detmath's general functions beyond them
+__device__ __noinline__ double dexp(double x) {
+    if (__builtin_fabs(x) <= 708.0) return gsb_exp(x, gsb_load());
+    return detmath::exp(x);
+}
+__device__ __noinline__ double dlog(double x) {
+    if (x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308) return gsb_log(x, gsb_load());
+    return detmath::log(x);
+}
+#else
 __device__ __noinline__ double dexp(double x) { return detmath::exp(x); }
 __device__ __noinline__ double dlog(double x) { return detmath::log(x); }
+#endif
 // two exps in one out-of-line call: the two Horner chains interleave (each one's fma latency hidden behind the
 // other's), where two calls would run them back to back; the same bits as two dexp calls
 struct dexp_pair {
@@ -32,6 +49,14 @@ struct dexp_pair {
 };
 __device__ __noinline__ dexp_pair dexp2(double x, double y) {
     dexp_pair r;
+#if SHYFT_TABLE_CALLS
+    if (__builtin_fabs(x) <= 708.0 && __builtin_fabs(y) <= 708.0) {
+        const gsb_k k = gsb_load();
+        r.a = gsb_exp(x, k);
+        r.b = gsb_exp(y, k);
+        return r;
+    }
+#endif
     if (__builtin_fabs(x) <= 708.0 && __builtin_fabs(y) <= 708.0) {
 #pragma clang fp contract(off)
         // detmath::exp_poly on both arguments, step by step side by side

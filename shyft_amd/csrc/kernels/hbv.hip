@@ -7,6 +7,9 @@
 // the collector series written [series][step][cell]. Wind speed is not read
 // (hbv_stack.h:295-301), so a step moves 32 B of forcing in and 16 B of
 // discharge/charge out per cell.
+// out-of-line exp / log with their constants from the SGPR table (device/special.h SHYFT_TABLE_CALLS): measured
+// r05 (ms per 730-step chunk, year mean) hbv_stack 7.75 -> 7.65; pt_gs_k keeps the default (80.9 -> 82.7 with the table)
+#define SHYFT_TABLE_CALLS 1
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -10,6 +10,9 @@
 // actual evapotranspiration (kirchner-q based, as pt_gs_k) -> kirchner (dopri5, shared with
 // pt_gs_k) -> total discharge / charge. 40 B of forcing in (wind is read by the reference's
 // accessor set but unused) and 16 B of discharge/charge out per cell-step.
+// out-of-line exp / log with their constants from the SGPR table (device/special.h SHYFT_TABLE_CALLS): measured
+// r05 (ms per 730-step chunk, year mean) pt_hs_k 34.3 -> 34.0; pt_gs_k keeps the default (80.9 -> 82.7 with the table)
+#define SHYFT_TABLE_CALLS 1
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -9,6 +9,9 @@
 // Per step: p_corr -> skaugen snow -> glacier melt on the post-step sca ->
 // Priestley-Taylor -> actual evapotranspiration -> kirchner (dopri5, shared with
 // pt_gs_k) -> total discharge / charge.
+// out-of-line exp / log with their constants from the SGPR table (device/special.h SHYFT_TABLE_CALLS): measured
+// r05 (ms per 730-step chunk, year mean) pt_ss_k 88.0 -> 87.1; pt_gs_k keeps the default (80.9 -> 82.7 with the table)
+#define SHYFT_TABLE_CALLS 1
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
