@@ -128,7 +128,8 @@ hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_step
                              const double* w, double* out, hipStream_t stream);
 
 // per-catchment sums: out[c][t] = sum over cells of segment c (seg_cells[seg_off[c]..seg_off[c+1]))
-// (w != null: sum of series * w[cell], the area-weighted sums of model_calibration.h:765-776)
+// (w != null: sum of series * w[cell], the area-weighted sums of model_calibration.h:765-776; seg_cells == null: the
+// identity, seg_cells[k] == k)
 hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
                                const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream,
                                const double* w = nullptr);

@@ -126,6 +126,9 @@ struct shyft_hip_region {
 
     // routing groups (cells sharing river + UHG): segment tables for the group discharge sums
     dbuf<int32_t> d_rseg_cells, d_rseg_off;
+    // the catchment / routing-group segments are the identity permutation of the cells (contiguous ranges in cell
+    // order): the segment sums do not read the index arrays
+    bool seg_identity = false, rseg_identity = false;
     size_t n_route_groups = 0;
 
     // parameter ensemble (calibration): a lane region of calculated cells x members that reads this

@@ -52,6 +52,10 @@ __global__ __launch_bounds__(RB) void select_sum_kernel(const double* __restrict
     if (threadIdx.x == 0) out[t] = r;
 }
 
+// ID: the segments' cells are the identity permutation (seg_cells[k] == k: catchments as contiguous cell ranges in
+// cell order), so the index array is not read (8 instead of 12 B per cell-step). Each lane loads four of its terms
+// ahead and adds them in its own order: the same sum as one term at a time, with four loads in flight.
+template <bool ID, bool W>
 __global__ __launch_bounds__(RB) void segment_sum_kernel(const double* __restrict__ series, size_t n_cells, size_t n_steps,
                                                          const int32_t* __restrict__ seg_cells,
                                                          const int32_t* __restrict__ seg_off, double* __restrict__ out,
@@ -61,10 +65,20 @@ __global__ __launch_bounds__(RB) void segment_sum_kernel(const double* __restric
     const double* __restrict__ row = series + t * n_cells;
     const int32_t b = seg_off[c], e = seg_off[c + 1];
     double acc = 0.0;
-    if (w) {
-        for (int32_t k = b + (int32_t)threadIdx.x; k < e; k += RB) acc += row[seg_cells[k]] * w[seg_cells[k]];
-    } else {
-        for (int32_t k = b + (int32_t)threadIdx.x; k < e; k += RB) acc += row[seg_cells[k]];
+    int32_t k = b + (int32_t)threadIdx.x;
+    for (; k + 3 * RB < e; k += 4 * RB) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int32_t i = ID ? k + u * RB : seg_cells[k + u * RB];
+            v[u] = W ? row[i] * w[i] : row[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    for (; k < e; k += RB) {
+        const int32_t i = ID ? k : seg_cells[k];
+        acc += W ? row[i] * w[i] : row[i];
     }
     const double r = block_sum(acc);
     if (threadIdx.x == 0) out[c * n_steps + t] = r;
@@ -125,8 +139,14 @@ hipError_t launch_select_sum(const double* series, size_t n_cells, size_t n_step
 hipError_t launch_segment_sums(const double* series, size_t n_cells, size_t n_steps, const int32_t* seg_cells,
                                const int32_t* seg_off, size_t n_seg, double* out, hipStream_t stream, const double* w) {
     if (n_steps == 0 || n_seg == 0) return hipSuccess;
-    hipLaunchKernelGGL(segment_sum_kernel, dim3((unsigned)n_steps, (unsigned)n_seg), dim3(RB), 0, stream, series, n_cells,
-                       n_steps, seg_cells, seg_off, out, w);
+    const dim3 grid((unsigned)n_steps, (unsigned)n_seg);
+    if (!seg_cells) {
+        if (w) hipLaunchKernelGGL((segment_sum_kernel<true, true>), grid, dim3(RB), 0, stream, series, n_cells, n_steps, seg_cells, seg_off, out, w);
+        else hipLaunchKernelGGL((segment_sum_kernel<true, false>), grid, dim3(RB), 0, stream, series, n_cells, n_steps, seg_cells, seg_off, out, w);
+    } else {
+        if (w) hipLaunchKernelGGL((segment_sum_kernel<false, true>), grid, dim3(RB), 0, stream, series, n_cells, n_steps, seg_cells, seg_off, out, w);
+        else hipLaunchKernelGGL((segment_sum_kernel<false, false>), grid, dim3(RB), 0, stream, series, n_cells, n_steps, seg_cells, seg_off, out, w);
+    }
     return hipGetLastError();
 }
 

@@ -122,6 +122,8 @@ void update_ix_to_id_mapping(shyft_hip_region* h) {
     for (size_t c = 0; c < C; ++c) off[c + 1] += off[c];
     std::vector<int32_t> pos(off.begin(), off.end() - 1);
     for (size_t i = 0; i < h->n; ++i) cells[pos[h->cix[i]]++] = int32_t(i);
+    h->seg_identity = true;
+    for (size_t i = 0; i < h->n && h->seg_identity; ++i) h->seg_identity = cells[i] == int32_t(i);
     h->d_seg_cells.alloc(h->n);
     h->d_seg_off.alloc(C + 1);
     hip_check(region_copy(h, h->d_seg_cells.p, cells.data(), h->n * sizeof(int32_t), hipMemcpyHostToDevice), "upload seg");
@@ -1355,7 +1357,7 @@ int shyft_hip_catchment_sums(const shyft_hip_region* hc, int series, size_t step
             h->d_tmp.alloc(std::max(h->d_tmp.n, C * n));
             out = h->d_tmp.p;
         }
-        hip_check(launch_segment_sums(src, h->n, n, h->d_seg_cells.p, h->d_seg_off.p, C, out, h->stream), "segment_sums");
+        hip_check(launch_segment_sums(src, h->n, n, h->seg_identity ? nullptr : h->d_seg_cells.p, h->d_seg_off.p, C, out, h->stream), "segment_sums");
         if (!dst_on_device) copy_rows(h->stream, dst, out, C * n * sizeof(double), 0, 1);
         else hip_check(hipStreamSynchronize(h->stream), "sync");
     });
@@ -1376,7 +1378,7 @@ int shyft_hip_catchment_area_sums(const shyft_hip_region* hc, int series, size_t
             h->d_tmp.alloc(std::max(h->d_tmp.n, C * n));
             out = h->d_tmp.p;
         }
-        hip_check(launch_segment_sums(src, h->n, n, h->d_seg_cells.p, h->d_seg_off.p, C, out, h->stream, w),
+        hip_check(launch_segment_sums(src, h->n, n, h->seg_identity ? nullptr : h->d_seg_cells.p, h->d_seg_off.p, C, out, h->stream, w),
                   "segment_sums");
         if (!dst_on_device) copy_rows(h->stream, dst, out, C * n * sizeof(double), 0, 1);
         else hip_check(hipStreamSynchronize(h->stream), "sync");
@@ -1434,6 +1436,7 @@ int shyft_hip_region_clone(const shyft_hip_region* src, shyft_hip_region** out) 
         clone_buf(h->d_doy, src->d_doy);
         clone_buf(h->d_trel, src->d_trel);
         clone_buf(h->d_seg_cells, src->d_seg_cells);
+        h->seg_identity = src->seg_identity;
         clone_buf(h->d_seg_off, src->d_seg_off);
         clone_buf(h->d_active, src->d_active);
         clone_buf(h->d_alt, src->d_alt);
@@ -1545,6 +1548,8 @@ int shyft_hip_set_routing_groups(shyft_hip_region* h, const int32_t* group_of_ce
         std::vector<int32_t> pos(off.begin(), off.end() - 1);
         for (size_t i = 0; i < h->n && n_groups; ++i)
             if (group_of_cell[i] >= 0) cells[size_t(pos[size_t(group_of_cell[i])]++)] = int32_t(i);
+        h->rseg_identity = cells.size() == h->n;
+        for (size_t i = 0; i < cells.size() && h->rseg_identity; ++i) h->rseg_identity = cells[i] == int32_t(i);
         h->d_rseg_off.alloc(n_groups + 1);
         h->d_rseg_cells.alloc(std::max<size_t>(1, cells.size()));
         hip_check(region_copy(h, h->d_rseg_off.p, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice), "upload");
@@ -1568,7 +1573,7 @@ int shyft_hip_routing_group_sums(const shyft_hip_region* hc, size_t step0, size_
             h->d_tmp.alloc(std::max(h->d_tmp.n, G * n));
             out = h->d_tmp.p;
         }
-        hip_check(launch_segment_sums(src, h->n, n, h->d_rseg_cells.p, h->d_rseg_off.p, G, out, h->stream),
+        hip_check(launch_segment_sums(src, h->n, n, h->rseg_identity ? nullptr : h->d_rseg_cells.p, h->d_rseg_off.p, G, out, h->stream),
                   "routing group sums");
         if (!dst_on_device) copy_rows(h->stream, dst, out, G * n * sizeof(double), 0, 1);
         else hip_check(hipStreamSynchronize(h->stream), "sync");
