@@ -283,7 +283,11 @@ enum shyft_hip_knob {
     SHYFT_HIP_KNOB_PTGSK_INSTANCE = 1, SHYFT_HIP_KNOB_BRENT_READ_DELAY = 2,
     /* sharded regions: 1 = run_cells runs the shards one after another (per-shard kernel times without contention,
      * shyft_hip_shard_run_ms); 0 = concurrently (the default) */
-    SHYFT_HIP_KNOB_SERIAL_SHARDS = 3
+    SHYFT_HIP_KNOB_SERIAL_SHARDS = 3,
+    /* sharded regions: k >= 0 makes the next shyft_hip_region_clone of this region fail when it reaches shard k (the
+     * shards before it already cloned, with their streams), so the clean-up of a partly built clone is exercised;
+     * the failure is reported like any other and disarms the knob; < 0 = off (the default) */
+    SHYFT_HIP_KNOB_CLONE_FAIL_AT = 4
 };
 int shyft_hip_set_test_knob(shyft_hip_region* h, int knob, int64_t value);
 

@@ -1499,8 +1499,8 @@ int shyft_hip_set_test_knob(shyft_hip_region* h, int knob, int64_t value) {
             if (value != 0 && value != 2 && value != 4)
                 throw std::runtime_error("set_test_knob: pt_gs_k instance must be 0 (auto), 2 or 4");
             h->knob_instance = int(value);
-        } else if (knob == SHYFT_HIP_KNOB_SERIAL_SHARDS) {
-            throw std::runtime_error("set_test_knob: serial shards needs a sharded region");
+        } else if (knob == SHYFT_HIP_KNOB_SERIAL_SHARDS || knob == SHYFT_HIP_KNOB_CLONE_FAIL_AT) {
+            throw std::runtime_error("set_test_knob: this knob needs a sharded region");
         } else if (knob == SHYFT_HIP_KNOB_BRENT_READ_DELAY) {
             if (value < 0 || value > 1000) throw std::runtime_error("set_test_knob: read delay must be in [0, 1000]");
             h->knob_read_delay = int(value);

@@ -58,6 +58,7 @@ struct shard_set {
     // SHYFT_HIP_SHARD_BALANCE_Z: the cells are dealt to the shards by elevation rank (fixed at the first set_geo), so
     // every shard holds the same mix of elevations; each shard keeps its cells in region order
     bool serial = false;                       // SHYFT_HIP_KNOB_SERIAL_SHARDS: run_cells one shard after another
+    mutable int64_t clone_fail_at = -1;        // SHYFT_HIP_KNOB_CLONE_FAIL_AT: the next clone fails at this shard
     bool permuted = false;
     std::vector<std::vector<int64_t>> cells;   // permuted: region cells of shard k, ascending
     std::vector<int32_t> cell_k, cell_j;       // permuted: region cell -> (shard, index in the shard)
@@ -442,6 +443,10 @@ const char* combine_report(const shard_set* s) { return s->report.c_str(); }
 void set_test_knob(shard_set* s, int knob, int64_t value) {
     if (knob == SHYFT_HIP_KNOB_SERIAL_SHARDS) {
         s->serial = value != 0;
+        return;
+    }
+    if (knob == SHYFT_HIP_KNOB_CLONE_FAIL_AT) {
+        s->clone_fail_at = value < 0 ? -1 : value;
         return;
     }
     for_shards(s, [&](size_t k) { ck(s->r[k], shyft_hip_set_test_knob(s->r[k], knob, value)); }, false);
@@ -859,7 +864,10 @@ shard_set* clone(const shard_set* src) {
     s->cells = src->cells;
     s->cell_k = src->cell_k;
     s->cell_j = src->cell_j;
+    const int64_t fail_at = src->clone_fail_at;
+    src->clone_fail_at = -1;
     for (size_t k = 0; k < src->S(); ++k) {
+        if (int64_t(k) == fail_at) throw std::runtime_error("clone: injected failure at shard " + std::to_string(k));
         hip_check(hipSetDevice(src->dev[k]), "hipSetDevice");
         shyft_hip_region* c = nullptr;
         if (shyft_hip_region_clone(src->r[k], &c)) throw std::runtime_error(shyft_hip_last_error(nullptr));

@@ -27,7 +27,7 @@ HBV_STATE = (("swe", "sca", "soil_moisture", "tank_uz", "tank_lz", "n_bins") +
              tuple(f"sp{i}" for i in range(HBV_MAX_BINS)) + tuple(f"sw{i}" for i in range(HBV_MAX_BINS)))
 SCOPE_CELL_IX, SCOPE_CATCHMENT = 0, 1
 SERIES_FORCING, SERIES_STATE = 100, 200
-KNOB_PTGSK_INSTANCE, KNOB_BRENT_READ_DELAY, KNOB_SERIAL_SHARDS = 1, 2, 3
+KNOB_PTGSK_INSTANCE, KNOB_BRENT_READ_DELAY, KNOB_SERIAL_SHARDS, KNOB_CLONE_FAIL_AT = 1, 2, 3, 4
 # shyft_hip_region_create_sharded_ex options (include/shyft_hip.h)
 SHARD_RCCL_ALWAYS, SHARD_NO_RCCL, SHARD_TEST_FAIL_INIT, SHARD_TEST_FAIL_GATHER, SHARD_TEST_CORRUPT_CHECK = 1, 2, 4, 8, 16
 SHARD_BALANCE_Z = 32

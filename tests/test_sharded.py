@@ -406,3 +406,41 @@ def test_balance_z_spreads_snow_work_and_keeps_results():
             sh.close()
     assert spread["balanced"] <= 0.10, spread
     assert spread["contiguous"] > 2 * spread["balanced"], spread
+
+
+def test_clone_failure_midway_cleans_up_and_leaves_the_source_usable():
+    """a clone that fails at shard k > 0 (shards before it cloned, their streams created) must report
+    the error and release what it built -- not crash in the clean-up -- and the source region keeps working."""
+    import ctypes as C
+    from shyft_amd.region import KNOB_CLONE_FAIL_AT
+    sh = _flagged(0, devices=(0, 0, 0))
+    try:
+        s0 = sh.get_state()
+        _run(sh)
+        before = sh.catchment_sums(0, 0, T), sh.get_series(0, 0, T)
+        for k in (2, 1, 0):
+            sh.set_test_knob(KNOB_CLONE_FAIL_AT, k)
+            h = C.c_void_p()
+            assert sh._L.shyft_hip_region_clone(sh.h, C.byref(h)) != 0
+            assert not h.value
+            assert f"injected failure at shard {k}" in sh._L.shyft_hip_last_error(None).decode()
+        # the knob disarms itself: the next clone builds, and the source still runs with unchanged results
+        h = C.c_void_p()
+        assert sh._L.shyft_hip_region_clone(sh.h, C.byref(h)) == 0 and h.value
+        sh._L.shyft_hip_region_destroy(h)
+        sh.set_state(s0)
+        _run(sh)
+        assert _same(sh.catchment_sums(0, 0, T), before[0]) and _same(sh.get_series(0, 0, T), before[1])
+    finally:
+        sh.close()
+
+
+def test_clone_fail_knob_needs_a_sharded_region():
+    from shyft_amd._native import ShyftHipError
+    from shyft_amd.region import KNOB_CLONE_FAIL_AT
+    r = _region("pt_gs_k", None)
+    try:
+        with pytest.raises(ShyftHipError, match="needs a sharded region"):
+            r.set_test_knob(KNOB_CLONE_FAIL_AT, 1)
+    finally:
+        r.close()
