@@ -79,7 +79,14 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     const size_t N = (size_t)a.n_cells;
     const size_t NF = ENS ? (size_t)a.f_cols : N;
     const size_t fcl = ENS ? (size_t)a.fcol[lc] : (size_t)lc;
-    const double* __restrict__ P = UNIFORM ? a.params : a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
+    const double* __restrict__ Pg = UNIFORM ? a.params : a.params + (size_t)a.set_ix[lc] * PTGSK_NP;
+    // the uniform parameter row in LDS (288 B next to the 38.9 KB of job queue and cell constants): the step loop
+    // reads it with ds_read_b64 where it is used instead of holding 36 doubles in SGPRs, which spilled to VGPR lanes
+    // (a v_readlane per use) beside the inline exp / log constant table. r05: 80.8 -> 79.0 ms per 730-step chunk,
+    // v_readlane_b32 326 -> 270 in the kernel's code. (Read after the first barrier below.)
+    __shared__ double lpar[UNIFORM ? PTGSK_NP : 1];
+    if (UNIFORM && threadIdx.x < PTGSK_NP) lpar[threadIdx.x] = a.params[threadIdx.x];
+    const double* __restrict__ P = UNIFORM ? (const double*)lpar : Pg;
 
     // per-cell constants (pt_gs_k.h:347-357)
     const double* __restrict__ cc = a.cellc;
@@ -152,9 +159,9 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
     const size_t RS = TW * N;  // stride between response series
     double* __restrict__ SS = a.state_series;
     const size_t SSS = (TW + 1) * N;
-    const int wed = (int)P[PK_WED];
-    const int64_t snow_lo = (int64_t)((int)(P[PK_WED] * 24) - (int)(P[PK_NWD] * 24)) * 3600000000LL;
-    const int64_t snow_hi = (int64_t)(int)(P[PK_WED] * 24) * 3600000000LL;
+    const int wed = (int)Pg[PK_WED];
+    const int64_t snow_lo = (int64_t)((int)(Pg[PK_WED] * 24) - (int)(Pg[PK_NWD] * 24)) * 3600000000LL;
+    const int64_t snow_hi = (int64_t)(int)(Pg[PK_WED] * 24) * 3600000000LL;
 
     // Brent job queue of the workgroup (COMPACT)
     // (jres is not aliased with a job array: a lane reads its result after the step's second barrier, and another
