@@ -12,4 +12,8 @@ timeout -k 10 300 python bench.py --stack pt_ss_k --gpus 1 --steps 60 --warmup 1
 cut -c1-250 gpurun_out/bench_r_c5.json
 timeout -k 10 600 python bench.py --stack pt_ss_k --gpus 1 --shards 8 --total-cells 8388608 --steps 60 --warmup 1 --no-cpu-baseline > gpurun_out/bench_r_c5_sh8.json 2> gpurun_out/bench_r_c5_sh8.err || { tail -5 gpurun_out/bench_r_c5_sh8.err; exit 1; }
 cut -c1-250 gpurun_out/bench_r_c5_sh8.json
+timeout -k 10 600 python bench.py --stack hbv_stack --gpus 1 --shards 8 --total-cells 4194304 --no-cpu-baseline > gpurun_out/bench_r_c4_sh8.json 2> gpurun_out/bench_r_c4_sh8.err || { tail -5 gpurun_out/bench_r_c4_sh8.err; exit 1; }
+cut -c1-250 gpurun_out/bench_r_c4_sh8.json
+timeout -k 10 300 python bench.py --idw --no-cpu-baseline > gpurun_out/bench_r_idw.json 2> gpurun_out/bench_r_idw.err || { tail -5 gpurun_out/bench_r_idw.err; exit 1; }
+cut -c1-250 gpurun_out/bench_r_idw.json
 echo BATCH_R2_DONE
