@@ -8,11 +8,12 @@
 
 namespace shyft_dev {
 
-// exp / log by the gamma_lean.h fast paths inline (SGPR constant table), the out-of-line general function only
-// beyond them -- the same bits as dexp / dlog. Whether inline or out-of-line calls are faster depends on the kernel's
-// register pressure, so the callers choose (template argument INL): measured (r05, same box, year means per
-// 730-step chunk) pt_gs_k 92.1 -> 90.0 ms with PT and Kirchner inline, but hbv_stack 7.7 -> 8.0 ms and pt_hs_k
-// 34.3 -> 37.9 ms, pt_ss_k unchanged -- so only pt_gs_k takes them inline.
+// exp / log by the device/fastmath.h fast paths inline (SGPR constant table), the out-of-line general function only
+// beyond them -- the same bits as dexp / dlog. Every stack takes them inline (template argument INL = true) since the
+// constants are loaded per call (kmath<true> below) and pt_gs_k's parameter row moved to LDS; measured r05 (ms per
+// 730-step chunk, year mean, same box): hbv_stack 7.45 -> 7.25, pt_ss_k 87.1 -> 86.65, pt_hs_k 33.95 -> 32.95,
+// pt_hps_k 67.65 -> 63.05. (With one table held across the whole call, hbv_stack and pt_hs_k had measured 3-10 %
+// slower: 54 SGPRs live beside the step loop's uniform values.)
 // mathematics of a kernel: out-of-line calls (INL = false) or inline fast paths (INL = true: exp_fast / log_fast)
 template <bool INL>
 struct kmath {

@@ -172,7 +172,7 @@ void hbv_run_kernel(const hbv_kargs a) {
 #ifdef SHYFT_ABLATE_PT  // instruction-budget ablation only (wrong results): no Priestley-Taylor
         const double pot_evap = (rad * 1e-4 + rel_hum * 1e-5 + temp * 1e-6) * pt_alpha;
 #else
-        const double pot_evap = pt_pot_evap(pt_albedo, pt_alpha, temp, rad, rel_hum) * 3600.0;
+        const double pot_evap = pt_pot_evap<true>(pt_albedo, pt_alpha, temp, rad, rel_hum) * 3600.0;
 #endif
         // hbv_actual_evapotranspiration::calculate_step (hbv_actual_evapotranspiration.h:32-38)
         const double snow_fraction = smax(sca, glacier_fraction);
