@@ -7,6 +7,7 @@
 // factors s[] (not the quantiles), and the melt-front interpolation sets sp[idx-1] = sp[idx].
 #pragma once
 #include "hbv_dev.h"
+#include "pt_dev.h"
 
 namespace shyft_dev {
 
@@ -112,12 +113,15 @@ __device__ inline double hps_step(const hps_par& p, double (&sp)[MB], double (&s
                 else albedo[i] = (min_albedo + p.fast_decay * (albedo[i] - min_albedo));
             }
     }
-    const double lw_in = (0.98 * sigma * dpowr(vapour_pressure / T_k, 6.87e-2) * dpow4(T_k));
+    // dpowr and dexp by the inline fast paths (device/pt_dev.h kmath<true>; the same bits): 63.35 -> 62.8 ms per
+    // 730-step chunk (r05)
+    const kmath<true> hkm;
+    const double lw_in = (0.98 * sigma * hkm.exp(6.87e-2 * hkm.log(vapour_pressure / T_k)) * dpow4(T_k));
     const double sst = smin(0.0, 1.16 * T - 2.09);
     double turb_term;
     if (sst > -HPS_TOL) turb_term = turb * (T + 1.7 * (vapour_pressure - 6.12)) - p.BB0;
     else
-        turb_term = (turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * dexp(0.103 * T - 0.186))) -
+        turb_term = (turb * (T - sst + 1.7 * (vapour_pressure - 6.132 * hkm.exp(0.103 * T - 0.186))) -
                      0.98 * sigma * dpow4(sst + 273.15));
     double delta_sh = -surface_heat;
     const double new_surface_heat = p.surface_magnitude * ice_heat * sst * 0.5;
