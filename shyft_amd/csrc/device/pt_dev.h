@@ -9,11 +9,12 @@
 namespace shyft_dev {
 
 // exp / log by the device/fastmath.h fast paths inline (SGPR constant table), the out-of-line general function only
-// beyond them -- the same bits as dexp / dlog. Every stack takes them inline (template argument INL = true) since the
+// beyond them -- the same bits as dexp / dlog. The stacks take them inline (template argument INL = true) since the
 // constants are loaded per call (kmath<true> below) and pt_gs_k's parameter row moved to LDS; measured r05 (ms per
-// 730-step chunk, year mean, same box): hbv_stack 7.45 -> 7.25, pt_ss_k 87.1 -> 86.65, pt_hs_k 33.95 -> 32.95,
-// pt_hps_k 67.65 -> 63.05. (With one table held across the whole call, hbv_stack and pt_hs_k had measured 3-10 %
-// slower: 54 SGPRs live beside the step loop's uniform values.)
+// 730-step chunk, year mean, same box): hbv_stack 7.45 -> 7.25, pt_hs_k 33.95 -> 32.95, pt_hps_k 67.65 -> 63.05.
+// pt_ss_k keeps the calls: inline measured 87.1 -> 86.65 but its VGPR spills 19 -> 23 raised the C5 line's HBM
+// traffic from 1.06x to 1.56x the algorithmic bytes. (With one table held across the whole call, hbv_stack and
+// pt_hs_k had measured 3-10 % slower: 54 SGPRs live beside the step loop's uniform values.)
 // mathematics of a kernel: out-of-line calls (INL = false) or inline fast paths (INL = true: exp_fast / log_fast)
 template <bool INL>
 struct kmath {

@@ -196,11 +196,11 @@ void ptssk_run_kernel(const ptssk_kargs a) {
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
         double ae_exp;  // actual_evapotranspiration's exp, evaluated beside Priestley-Taylor's (pt_pot_evap_exp)
-        const double pot_evap = pt_pot_evap_exp<true>(pt_albedo, pt_alpha, temp, rad, rel_hum, -q * 3.0 / ae_scale, ae_exp) * 3600.0;
+        const double pot_evap = pt_pot_evap_exp(pt_albedo, pt_alpha, temp, rad, rel_hum, -q * 3.0 / ae_scale, ae_exp) * 3600.0;
         const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(s.sca, glacier_fraction));
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         double q_avg;
-        if (!kirchner_step<true>(q, q_avg, snow_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
+        if (!kirchner_step(q, q_avg, snow_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
                            ae, a.t1_hours, kc1, kc2, kc3))
             err = ERR_KIRCHNER_MAX_ITER;
         const double total_discharge = smax(0.0, prec - ae) * direct_response_fraction + gm_direct * gm_mmh +
