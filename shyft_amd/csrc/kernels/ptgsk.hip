@@ -360,11 +360,11 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
 
 // The step's out-of-line device functions (dexp / dexp2 / dlog / dlgamma, the Brent job) are shared by every
 // kernel of this file, and the AMDGPU attributor compiles a shared callee for the range of its callers' occupancy.
-// This never-launched caller makes that range tight: the callees are register-allocated for its occupancy, so they
-// clobber fewer registers across their calls. Measured (1M-cell bench year, 730-step chunks, bit-exact,
-// tools/ptgsk_variants.py): 8 waves (64 VGPRs) 105.3 -> 100.0 ms per chunk on the r03 kernel; on the r05 kernel
-// 8 waves 78.3, 7: 79.3, 6: 77.5, 5: 77.3, 4: 79.0, 3: 78.8 -- 5 waves (96 VGPRs; profiles/r05/variants_budget_ap.txt).
-__global__ __launch_bounds__(256, 5) void ptgsk_callee_budget_kernel(const ptgsk_kargs a) {
+// This never-launched 8-wave caller makes that range tight: the callees are register-allocated for 64 VGPRs, so
+// they clobber fewer registers and the 4-wave step loop keeps more values live across its calls (VGPR spills of
+// the bench instance 164 -> 127). Measured on the 1M-cell bench year, 730-step chunks: 105.3 -> 100.0 ms per chunk,
+// bit-exact (tools/ptgsk_variants.py).
+__global__ __launch_bounds__(256, 8) void ptgsk_callee_budget_kernel(const ptgsk_kargs a) {
     if (a.n_cells >= 0) return;  // never runs: launch_ptgsk_run only references it
     const int c = threadIdx.x;
     gs_state s{};
