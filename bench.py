@@ -161,20 +161,19 @@ FP64_PEAK_FLOPS = 78.6e12        # MI355X FP64 matrix/vector peak (AMD spec shee
 
 def launch_ranks(n_gpus):
     """`bench.py --gpus N` started without a launcher: this parent process starts N fresh rank processes
-    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, 127.0.0.1 rendezvous) and exits
-    with the first failing rank's status. The parent never touches the GPU (no torch import), so no
-    process that initialised HIP is replaced; a rank that fails takes the others down instead of leaving
-    them blocked in a collective."""
-    import socket
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, 127.0.0.1 rendezvous) and exits with the first
+    failing rank's status. Each rank is a supervisor (shyft_amd/supervise.py) that runs the real rank as its child and
+    falls back from RCCL to gloo combines if an attempt fails or stalls; the parent never touches the GPU and, as a last
+    resort, ends everything at a wall deadline (SHYFT_LAUNCH_DEADLINE_S, default 3600 s)."""
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    from shyft_amd.supervise import _free_port
+    port = _free_port()
+    deadline = time.monotonic() + float(os.environ.get("SHYFT_LAUNCH_DEADLINE_S", "3600"))
     procs = []
     for r in range(n_gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_gpus), LOCAL_WORLD_SIZE=str(n_gpus),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # rank 0's supervisor hosts the store
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
     live = list(procs)
@@ -188,8 +187,18 @@ def launch_ranks(n_gpus):
                 rc = code
                 for q in live:
                     q.terminate()
+        if live and time.monotonic() > deadline:
+            print("bench.py: launcher wall deadline reached, ending the ranks", file=sys.stderr, flush=True)
+            for q in live:
+                q.kill()
+            rc = rc or 124
         time.sleep(0.05)
     return rc
+
+
+def _progress(name):
+    from shyft_amd.supervise import progress
+    progress(name)
 
 
 def dist_setup(n_gpus, use_gpu=True):
@@ -215,20 +224,31 @@ def dist_setup(n_gpus, use_gpu=True):
                                  f"(SHYFT_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
             local = local % n_dev if n_dev else local
             torch.cuda.set_device(local)
+        from datetime import timedelta
+        # a deadline on the rendezvous and on every collective (gloo raises, RCCL's watchdog aborts), below the
+        # supervisor's stall limit, so that a stalled exchange ends this attempt rather than the whole run
+        timeout = timedelta(seconds=float(os.environ.get("SHYFT_DIST_TIMEOUT_S", "180")))
         try:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
         except Exception:  # noqa: BLE001 -- a torch without mixed-backend groups: RCCL alone (no host fallback)
             if backend != "cpu:gloo,cuda:nccl":
                 raise
-            dist.init_process_group("nccl")
+            dist.init_process_group("nccl", timeout=timeout)
         assert dist.get_world_size() == n_gpus
+        _progress("rendezvous")
         pg = dist
+        stall = os.environ.get("SHYFT_DIST_TEST_STALL", "")   # "rank:attempt": that rank stalls in the self-check
+        if stall and stall == f"{rank}:{os.environ.get('SHYFT_SUPERVISE_ATTEMPT', '0')}":
+            time.sleep(3600)   # (tests/test_bench_launch.py: the supervisor must replace this attempt)
+        # one known-value all-gather, bit-exact on every rank, before any data uses the combines' path
+        from shyft_amd import distributed
+        nccl = "nccl" in str(dist.get_backend())
         if use_gpu:
-            # one known-value all-gather, bit-exact on every rank, before any data uses RCCL
-            from shyft_amd import distributed
             import torch
-            nccl = "nccl" in str(dist.get_backend())
             distributed.verify_collectives(device=torch.device("cuda", local) if nccl else None)
+        else:
+            distributed.verify_collectives()
+        _progress("self-check")
     return world, rank, local, pg
 
 
@@ -402,6 +422,7 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
         return _run_year_overlapped(r, L, chunk, k_steps, seed, router, sums, walls, parts, overlap)
     kernel_ms = []
     for s in range(k_steps):
+        _progress(f"chunk {s}")
         t_chunk = time.perf_counter()
         step0 = s * chunk
         # the chunk's forcing rows are all rewritten below and run_cells writes every response row of the
@@ -450,6 +471,7 @@ def _run_year_overlapped(r, L, chunk, k_steps, seed, router, sums, walls, parts,
     r.move_window(0, 0)
     r.synthetic_forcing(seed, 0, chunk, cell_offset=L.off)
     for s in range(k_steps):
+        _progress(f"chunk {s}")
         t_chunk = time.perf_counter()
         step0 = s * chunk
         if s + 1 < k_steps:
@@ -592,9 +614,21 @@ def dist_check(a, world, rank, pg):
         print(json.dumps({"dist_check": True, "n_gpus": world, "backend": pg.get_backend() if pg else None,
                           "cells": L.total, "catchments": L.n_catch, "max_over_ranks": wall,
                           "max_abs_diff": float(np.abs(total - ref).max()),
-                          "checksum": float(total.sum())}), flush=True)
+                          "checksum": float(total.sum()), "combine": distributed.combine_report(),
+                          "supervisor": supervisor_info()}), flush=True)
     if pg is not None:
         pg.destroy_process_group()
+
+
+def supervisor_info():
+    """The `supervisor` field of a rank's line: which attempt produced it and why the one before ended."""
+    if os.environ.get("SHYFT_SUPERVISED") != "1":
+        return None
+    return {"attempt": int(os.environ.get("SHYFT_SUPERVISE_ATTEMPT", "0")),
+            "combines": os.environ.get("SHYFT_SUPERVISE_MODE", ""),
+            "previous_attempt": os.environ.get("SHYFT_SUPERVISE_REASON", "") or None,
+            "note": "each rank process supervises its rank as a child and restarts all ranks with gloo combines if "
+                    "the RCCL attempt fails or stalls (shyft_amd/supervise.py)"}
 
 
 def main():
@@ -604,6 +638,16 @@ def main():
     engine = "WORLD_SIZE" not in os.environ and a.launch == "engine" and not a.dist_check
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not engine:
         sys.exit(launch_ranks(a.gpus))
+    if "WORLD_SIZE" in os.environ and not engine and int(os.environ["WORLD_SIZE"]) != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: the line would not "
+                         f"measure {a.gpus} GPU(s)")
+    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("SHYFT_SUPERVISED") != "1"
+            and os.environ.get("SHYFT_NO_SUPERVISE") != "1"):
+        # a rank process (torch.distributed.run's or launch_ranks'): supervise the real rank as a child. Nothing here
+        # has touched the GPU.
+        from shyft_amd.supervise import supervise
+        sys.exit(supervise([sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    _progress("start")
     devices = None
     if engine and (a.gpus > 1 or a.shards > 1):
         # one process, the region's cells in shards over the GPUs (the engine's multi-GPU path)
@@ -621,6 +665,7 @@ def main():
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
     from shyft_amd.region import SHARD_BALANCE_Z
     r = build_region(a.stack, L, local, chunk, n_axis, devices, SHARD_BALANCE_Z if a.balance_z else 0)
+    _progress("region")
     state0 = stack_defaults(a.stack, L.n)[1]
     read_b, write_b, state_b, kernel_name = STACKS[a.stack]
     stations = None
@@ -798,6 +843,8 @@ def main():
                                          "the timed region)"}
         if a.dump_sums and rank == 0:
             np.save(a.dump_sums, tot.cpu().numpy())
+    if supervisor_info() is not None:
+        out["supervisor"] = supervisor_info()
     if rank == 0 and world == 1 and not devices and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         out["cpu_baseline"] = cpu_baseline(a.stack, a.cpu_cells, threads)

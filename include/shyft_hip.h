@@ -82,11 +82,14 @@ int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* device
 /* create_sharded with options. The combine path is chosen once, at creation: RCCL when every shard has its own
  * device (or with SHYFT_HIP_SHARD_RCCL_ALWAYS: also one shard, a one-rank communicator), then a self-check before any
  * data uses it -- an all-gather of known partials must arrive bit for bit on every device and their shard-order sum
- * must equal the device-copy path's bitwise. A failed ncclCommInitAll, a failed self-check, or an RCCL error at run
- * time switches the region to device copies (same results; shyft_hip_region_combine_report says why). No reference
+ * must equal the device-copy path's bitwise. A failed communicator initialisation, a failed self-check, or an RCCL error
+ * at run time switches the region to device copies (same results; shyft_hip_region_combine_report says why). Every
+ * RCCL step has a deadline (SHYFT_HIP_RCCL_DEADLINE_MS, default 120 s; non-blocking communicators, polled): one that
+ * stalls is aborted (ncclCommAbort) and handled like one that fails. No reference
  * counterpart: the reference's one-process region has no exchange (core/region_model.h:972-1021).
  * SHYFT_HIP_SHARD_NO_RCCL: device copies only. The TEST_ flags inject the failures for the fallback tests:
- * ncclCommInitAll failing, the first all-gather after the self-check failing, the self-check comparing unequal.
+ * ncclCommInitAll failing, the first all-gather after the self-check failing, the self-check comparing unequal, the
+ * self-check's all-gather not seen to complete before the deadline (TEST_STALL_CHECK).
  * SHYFT_HIP_SHARD_BALANCE_Z: instead of contiguous cell ranges, the first shyft_hip_set_geo ranks the cells by
  * elevation and deals rank r to shard r % n_shards (each shard keeps its cells in region order), so every shard holds
  * the same mix of elevations and so of snow-season work. Every entry point still takes the region's cell indexes;
@@ -95,7 +98,8 @@ int shyft_hip_region_create_sharded(int stack, size_t n_cells, const int* device
  * position in the deal). */
 enum shyft_hip_shard_flags {
     SHYFT_HIP_SHARD_RCCL_ALWAYS = 1, SHYFT_HIP_SHARD_NO_RCCL = 2, SHYFT_HIP_SHARD_TEST_FAIL_INIT = 4,
-    SHYFT_HIP_SHARD_TEST_FAIL_GATHER = 8, SHYFT_HIP_SHARD_TEST_CORRUPT_CHECK = 16, SHYFT_HIP_SHARD_BALANCE_Z = 32
+    SHYFT_HIP_SHARD_TEST_FAIL_GATHER = 8, SHYFT_HIP_SHARD_TEST_CORRUPT_CHECK = 16, SHYFT_HIP_SHARD_BALANCE_Z = 32,
+    SHYFT_HIP_SHARD_TEST_STALL_CHECK = 64
 };
 int shyft_hip_region_create_sharded_ex(int stack, size_t n_cells, const int* devices, size_t n_shards, unsigned flags,
                                        shyft_hip_region** out);

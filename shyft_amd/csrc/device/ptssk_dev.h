@@ -70,25 +70,106 @@ __device__ __forceinline__ ss_pdf_pair ss_gamma_pdf2(double nu_m, double nu_a, d
 
 __device__ inline double ss_c(uint64_t n, double d_range) { return dexp(-(double)n / d_range); }
 
-// statistics::sca_rel_red (skaugen.h:57-82)
-__device__ __noinline__ double ss_sca_rel_red(uint64_t u, uint64_t n, double nu_a, double alpha, int32_t& err) {
+// zero_func's value at x (ss_gamma_pdf2: pdf_m - pdf_a), or -1.0 / +1.0 where its sign is certain without the four
+// divisions: pdf = exp(.) / z / theta with the same z > 0 and theta > 0 for both, and correctly rounded division is
+// monotonic, so exp_m < exp_a by more than 2^-48 relative gives pdf_m < pdf_a, a negative, non-zero difference: the
+// larger quotient is normal (exp_a, z and theta far from the ends of the range), each of its two roundings moves it by
+// at most 2^-53 relative, and the smaller one -- normal, subnormal or zero -- stays below it. Two exps that underflowed
+// to 0 give 0, as the divisions do (the bisection then stops at that midpoint, as the reference's does).
+// The bisection looks only at the sign of its midpoint values and whether they are zero (its one product test
+// uses the exact opening values), so its sequence of brackets is unchanged.
+__device__ __forceinline__ double ss_zero_sign(double nu_m, double nu_a, double theta, double lg_m, double lg_a,
+                                               double x, int32_t& err) {
+    if (x == 0) {
+        const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, x, err);
+        return f.m - f.a;
+    }
+    const double z = x / theta;
+    const double lz = dlog(z);
+    const dexp_pair e = dexp2(nu_m * lz - z - lg_m, nu_a * lz - z - lg_a);
+    if (e.a == 0 && e.b == 0) return 0.0;  // both pdfs underflowed: 0 / z / theta - 0 / z / theta
+    const double LO = 0x1p-960, HI = 0x1p960;  // the larger exp normal, far from both ends: so is its pdf
+    if (z >= 0x1p-30 && z <= 0x1p30 && theta >= 0x1p-30 && theta <= 0x1p30) {
+        if (e.b >= LO && e.b <= HI && e.b > e.a * (1.0 + 0x1p-48)) return -1.0;
+        if (e.a >= LO && e.a <= HI && e.a > e.b * (1.0 + 0x1p-48)) return 1.0;
+    }
+    return e.a / z / theta - e.b / z / theta;  // ss_gamma_pdf2's divisions, in its order
+}
+
+// x == 0 is the only point where either pdf of zero_func raises (the pole of a shape < 1, ss_gamma_pdf)
+__device__ __forceinline__ bool ss_pdf_pole(double x, double nu_m, double nu_a) { return x == 0 && (nu_m < 1 || nu_a < 1); }
+
+// value v of lane k of this lane's group of L consecutive lanes (L a power of two <= 64; the group's lanes run the
+// same control flow, so every source lane is active)
+__device__ __forceinline__ double grp_get(double v, int L, int k) {
+    return __shfl(v, (int)(__lane_id() & ~(unsigned)(L - 1)) + k, 64);
+}
+__device__ __forceinline__ int grp_get_i(int v, int L, int k) {
+    return __shfl(v, (int)(__lane_id() & ~(unsigned)(L - 1)) + k, 64);
+}
+
+// statistics::sca_rel_red (skaugen.h:57-82), evaluated by one lane (G = false) or by a group of L lanes (G = true,
+// L = 2 or 4, the same on every lane of a wavefront; k = this lane's index in its group; all L lanes pass the same
+// job and return the same value). The result is the sequential algorithm's, bit for bit: every zero_func value it
+// uses is the one the sequential algorithm computes at the same point, by the same code.
+//  - the 2-bit brent_find_minima stops at its first test for any finite positive bracket (|x - mid| = max/2 <=
+//    fract2 - max/2 = max/2 + 1/4): its one evaluation, f(max), is the bisection's f(upper) -- the Brent keeps
+//    fx = f(x) and returns x -- so the bisection does not evaluate it again;
+//  - the bracket walk's last test evaluates both pdfs at the final `lower`, which is the bisection's f(lower);
+//  - groups: lgamma(nu_m) / lgamma(nu_a), the two opening evaluations (f(max), and the walk's first test at the
+//    mean of g_m) and the two final cdfs run on lanes 0 / 1 side by side;
+//  - L = 4: the bisection evaluates the midpoints of the next 2 levels at once, one per lane (each point computed
+//    from the bracket by the same midpoint additions the sequential loop performs on the way there), and the group
+//    then replays the sequential loop over those levels -- its tests, its branch and its error on a pole at the
+//    points the sequential loop would have evaluated; the other point is discarded, with anything it raised.
+//    (tools/mb/ptssk_group_emu.cpp replays this on the 1M recorded jobs of a year against the oracle's bisect.)
+// Groups of 8 lanes (3 levels per round: the same replay, checked by the same emulation) faulted the GPU with a
+// memory-aperture violation in r06 (gpurun_out of the r06a variant run); the kernel caps L at 4.
+template <bool G>
+__device__ __forceinline__ double ss_sca_rel_red_body(uint64_t u, uint64_t n, double nu_a, double alpha, int L, int k,
+                                                      int32_t& err) {
     const double nu_m = ((double)u / n) * nu_a;
     const double theta = 1.0 / alpha;
-    const double lg_m = dlgamma(nu_m), lg_a = dlgamma(nu_a);
+    double lg_m, lg_a;
+    if (!G) {
+        lg_m = dlgamma(nu_m);
+        lg_a = dlgamma(nu_a);
+    } else {
+        const double lg = dlgamma(k == 1 ? nu_a : nu_m);
+        lg_m = grp_get(lg, L, 0);
+        lg_a = grp_get(lg, L, 1);
+    }
     const double g_a_mean = nu_a * theta;
     auto zero_func = [&](double x) {
         const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, x, err);
         return f.m - f.a;
     };
     double lower = nu_m * theta;
+    // the opening evaluations: Brent's f(max), and the walk's first test f(lower) (pdf_m < pdf_a: walk on)
+    double fx, f_low;
+    bool walk_on;
+    if (!G) {
+        fx = zero_func(g_a_mean);
+        const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, lower, err);
+        walk_on = f.m < f.a;
+        f_low = f.m - f.a;
+    } else {
+        int32_t e_spec = 0;  // both points are used: their poles are raised below
+        const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, k == 0 ? g_a_mean : lower, e_spec);
+        const double d = f.m - f.a;
+        fx = grp_get(d, L, 0);
+        f_low = grp_get(d, L, 1);
+        walk_on = grp_get_i(f.m < f.a ? 1 : 0, L, 1) != 0;
+        if (ss_pdf_pole(g_a_mean, nu_m, nu_a) || ss_pdf_pole(lower, nu_m, nu_a)) err = ERR_SKAUGEN_PDF;
+    }
     double upper;
     {  // brent_find_minima(zero_func, 0, g_a_mean, 2 bits), boost tools/minima.hpp
         double min = 0.0, max = g_a_mean;
         const double tolerance = 0.5;  // ldexp(1, 1-2)
         const double golden = (double)0.3819660f;
-        double x, w, v, uu, delta, delta2, fu, fv, fw, fx, mid, fract1, fract2;
+        double x, w, v, uu, delta, delta2, fu, fv, fw, mid, fract1, fract2;
         x = w = v = max;
-        fw = fv = fx = zero_func(x);
+        fw = fv = fx;
         delta2 = delta = 0;
         uint64_t count = ~uint64_t(0);
         do {
@@ -132,19 +213,29 @@ __device__ __noinline__ double ss_sca_rel_red(uint64_t u, uint64_t n, double nu_
                 }
             }
         } while (--count);
-        upper = x;
+        upper = x;  // fx = f(upper)
     }
     // while (pdf(g_m, lower) < pdf(g_a, lower)) lower *= 0.9; -- 0.9^k underflows to 0 within 7100 steps
-    for (int it = 0; it < 8000; ++it) {
-        const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, lower, err);
-        if (!(f.m < f.a)) break;
+    double fmin = f_low;
+    bool have_fmin = true;
+    if (walk_on) {
         lower *= 0.9;
+        have_fmin = false;
+        for (int it = 1; it < 8000; ++it) {
+            const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, lower, err);
+            if (!(f.m < f.a)) {
+                fmin = f.m - f.a;
+                have_fmin = true;
+                break;
+            }
+            lower *= 0.9;
+        }
     }
     // bisect(zero_func, lower, upper, eps_tolerance(10), max_iter = 100), boost tools/roots.hpp
     double bmin = lower, bmax = upper;
     {
-        double fmin = zero_func(bmin);
-        double fmax = zero_func(bmax);
+        if (!have_fmin) fmin = zero_func(bmin);
+        const double fmax = fx;
         if (fmin == 0) {
             bmax = bmin;
         } else if (fmax == 0) {
@@ -154,30 +245,95 @@ __device__ __noinline__ double ss_sca_rel_red(uint64_t u, uint64_t n, double nu_
         } else {
             const double eps = 0x1p-9;  // max(ldexp(1, 1-10), 4*DBL_EPSILON)
             int count = 97;             // max_iter 100 minus the three evaluations so far
-            while (count && !(fabs(bmin - bmax) <= eps * smin(fabs(bmin), fabs(bmax)))) {
-                const double mid = (bmin + bmax) / 2;
-                const double fmid = zero_func(mid);
-                if ((mid == bmax) || (mid == bmin)) break;
-                if (fmid == 0) {
-                    bmin = bmax = mid;
-                    break;
+            auto go_on = [&]() { return count && !(fabs(bmin - bmax) <= eps * smin(fabs(bmin), fabs(bmax))); };
+            if (!G || L < 4) {
+                while (go_on()) {
+                    const double mid = (bmin + bmax) / 2;
+                    const double fmid = ss_zero_sign(nu_m, nu_a, theta, lg_m, lg_a, mid, err);
+                    if ((mid == bmax) || (mid == bmin)) break;
+                    if (fmid == 0) {
+                        bmin = bmax = mid;
+                        break;
+                    }
+                    const int sm = fmid > 0 ? 1 : (fmid < 0 ? -1 : 0), sn = fmin > 0 ? 1 : (fmin < 0 ? -1 : 0);
+                    if (sm * sn < 0) {
+                        bmax = mid;
+                    } else {
+                        bmin = mid;
+                        fmin = fmid;
+                    }
+                    --count;
                 }
-                const int sm = fmid > 0 ? 1 : (fmid < 0 ? -1 : 0), sn = fmin > 0 ? 1 : (fmin < 0 ? -1 : 0);
-                if (sm * sn < 0) {
-                    bmax = mid;
-                    fmax = fmid;
-                } else {
-                    bmin = mid;
-                    fmin = fmid;
+            } else {
+                constexpr int D = 2;  // levels per round: 2^D - 1 <= L points
+                // this lane's point: heap node h (1 = the next midpoint, 2h / 2h+1 = the midpoints of its left /
+                // right half); lanes beyond the tree repeat the root
+                const int h = k < (1 << D) - 1 ? k + 1 : 1;
+                const int depth = 31 - __builtin_clz((unsigned)h);
+                bool more = go_on();
+                while (more) {
+                    double lo = bmin, hi = bmax;
+                    for (int b = depth - 1; b >= 0; --b) {
+                        const double m2 = (lo + hi) / 2;
+                        if ((h >> b) & 1) lo = m2; else hi = m2;
+                    }
+                    int32_t e_spec = 0;  // raised below for the points the sequential loop evaluates
+                    const double fk = ss_zero_sign(nu_m, nu_a, theta, lg_m, lg_a, (lo + hi) / 2, e_spec);
+                    int node = 1;
+                    for (int lev = 0; lev < D; ++lev) {
+                        if (lev > 0 && !go_on()) {
+                            more = false;
+                            break;
+                        }
+                        const double mid = (bmin + bmax) / 2;
+                        const double fmid = grp_get(fk, L, node - 1);
+                        if (ss_pdf_pole(mid, nu_m, nu_a)) err = ERR_SKAUGEN_PDF;
+                        if ((mid == bmax) || (mid == bmin)) {
+                            more = false;
+                            break;
+                        }
+                        if (fmid == 0) {
+                            bmin = bmax = mid;
+                            more = false;
+                            break;
+                        }
+                        const int sm = fmid > 0 ? 1 : (fmid < 0 ? -1 : 0), sn = fmin > 0 ? 1 : (fmin < 0 ? -1 : 0);
+                        if (sm * sn < 0) {
+                            bmax = mid;
+                            node = 2 * node;
+                        } else {
+                            bmin = mid;
+                            fmin = fmid;
+                            node = 2 * node + 1;
+                        }
+                        --count;
+                    }
+                    if (more) more = go_on();
                 }
-                --count;
             }
         }
     }
     const double x = (bmin + bmax) * 0.5;
-    const double m = gamma_p_prefix(nu_m, x / theta, lg_m, 2.220446049250313e-16).p;
-    const double a = gamma_p_prefix(nu_a, x / theta, lg_a, 2.220446049250313e-16).p;
+    double m, a;
+    if (!G) {
+        m = gamma_p_prefix(nu_m, x / theta, lg_m, 2.220446049250313e-16).p;
+        a = gamma_p_prefix(nu_a, x / theta, lg_a, 2.220446049250313e-16).p;
+    } else {
+        const double pk = gamma_p_prefix(k == 1 ? nu_a : nu_m, x / theta, k == 1 ? lg_a : lg_m, 2.220446049250313e-16).p;
+        m = grp_get(pk, L, 0);
+        a = grp_get(pk, L, 1);
+    }
     return a + 1.0 - m;
+}
+
+// one lane per job
+__device__ __noinline__ double ss_sca_rel_red(uint64_t u, uint64_t n, double nu_a, double alpha, int32_t& err) {
+    return ss_sca_rel_red_body<false>(u, n, nu_a, alpha, 1, 0, err);
+}
+// a group of L = 2 or 4 lanes per job
+__device__ __noinline__ double ss_sca_rel_red_group(uint64_t u, uint64_t n, double nu_a, double alpha, int L, int k,
+                                                    int32_t& err) {
+    return ss_sca_rel_red_body<true>(u, n, nu_a, alpha, L, k, err);
 }
 
 // calculator::compute_shape_vars (skaugen.h:338-380)

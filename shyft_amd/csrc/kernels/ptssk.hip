@@ -23,6 +23,25 @@
 
 using namespace shyft_dev;
 
+#ifdef SHYFT_PROF
+// phase timing (profiling builds only, tools/ptssk_phases.py): per-wavefront s_memtime deltas summed over the launch;
+// [0..4] front / queue + first barrier / job compute / second barrier / back + PT + AE + kirchner + stores,
+// [8] solver-wavefront job cycles, [9] solver wavefront-steps, [10] job lanes of those wavefront-steps
+__device__ unsigned long long g_ptssk_prof[12];
+extern "C" int shyft_ptssk_prof_read(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptssk_prof), sizeof(g_ptssk_prof)) != hipSuccess) return 1;
+    unsigned long long z[12] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ptssk_prof), z, sizeof z) != hipSuccess;
+}
+#define PROF_DECL unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long prof_t = __builtin_amdgcn_s_memtime();
+#define PROF_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[k] += t_ - prof_t; prof_t = t_; } while (0)
+#define PROF_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 6; ++k_) atomicAdd(&g_ptssk_prof[k_], prof_acc[k_]); } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(k) ((void)0)
+#define PROF_FLUSH() ((void)0)
+#endif
+
 namespace {
 
 constexpr int BLOCK = 256;
@@ -39,6 +58,24 @@ constexpr int BLOCK = 256;
 // (the same function of the same arguments: bit-identical to the per-lane call).
 // The solving wavefronts run at issue priority 3 (measured: 135.3 -> 134.5 ms per chunk).
 constexpr int JOB_PRIO = 3;
+
+// r06: a step with few jobs gives each job a group of L lanes of the solving wavefronts (ss_sca_rel_red<L>,
+// device/ptssk_dev.h: lgammas, opening evaluations and final cdfs side by side, the bisection 2-3 levels per
+// round), as long as the step's jobs fit GROUP_LANES lanes; the same bits as one lane per job
+#ifndef SHYFT_PTSSK_GROUP_LANES
+#define SHYFT_PTSSK_GROUP_LANES 64
+#endif
+#ifndef SHYFT_PTSSK_GROUP_MAX_L
+#define SHYFT_PTSSK_GROUP_MAX_L 4
+#endif
+static_assert(SHYFT_PTSSK_GROUP_MAX_L <= 4, "groups of 8 lanes faulted the GPU (device/ptssk_dev.h)");
+// a step with at least SELF_MIN jobs: every lane solves its own job, no queue and no second barrier (0: never)
+#ifndef SHYFT_PTSSK_SELF_MIN
+#define SHYFT_PTSSK_SELF_MIN 0
+#endif
+constexpr int SELF_MIN = SHYFT_PTSSK_SELF_MIN;
+constexpr int GROUP_LANES = SHYFT_PTSSK_GROUP_LANES;
+constexpr int GROUP_MAX_L = SHYFT_PTSSK_GROUP_MAX_L;
 
 // The 7 per-cell constants live in LDS (14 KB per workgroup next to the 11 KB job queue) instead of VGPRs live
 // across the sca_rel_red phase (as in the pt_gs_k kernel).
@@ -61,11 +98,16 @@ void ptssk_run_kernel(const ptssk_kargs a) {
     __shared__ uint64_t ju[BLOCK], jn[BLOCK];
     __shared__ double jnu[BLOCK], jal[BLOCK], jres[BLOCK];
     __shared__ int32_t jerr[BLOCK];
-    __shared__ int jcount[2];
+    // job counters, one per step in rotation (cb = step % 3): thread 0 zeroes the NEXT step's counter before this
+    // step's first barrier, and a counter is zeroed again only two steps after its step, when every wavefront has
+    // passed that step's first barrier and read it (a step without a second barrier -- no jobs, or every lane
+    // solving its own -- lets thread 0 run ahead by at most one step)
+    __shared__ int jcount[3];
     if (COMPACT) {
-        if (threadIdx.x == 0) jcount[0] = jcount[1] = 0;  // both: the first step may be odd (start_step)
+        if (threadIdx.x == 0) jcount[0] = jcount[1] = jcount[2] = 0;
         __syncthreads();
     }
+    int cb = 0;
 
     ss_par sp;
     sp.alpha_0 = P[SK_ALPHA0];
@@ -147,6 +189,7 @@ void ptssk_run_kernel(const ptssk_kargs a) {
     const int jrot = solver_lane0<BLOCK>(wsimd);
 
     const int i_end = a.step0 + a.n_steps;
+    PROF_DECL
     for (int i = a.step0; i < i_end; ++i) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
@@ -161,25 +204,60 @@ void ptssk_run_kernel(const ptssk_kargs a) {
         ss_front(sp, a.step_in_days, a.dt_hours, temp, prec, s, m, snow_outflow, snow_sca, snow_swe);
         if (!valid) m.need = false;
         double rel = 0.0;
+        PROF_MARK(0);
         if (COMPACT) {
-            if (threadIdx.x == 0) jcount[(i + 1) & 1] = 0;  // next step's counter (as in the pt_gs_k kernel)
+            const int nb = cb == 2 ? 0 : cb + 1;
+            if (threadIdx.x == 0) jcount[nb] = 0;  // next step's counter
             int slot = -1;
             if (m.need) {
-                slot = atomicAdd(&jcount[i & 1], 1);
+                slot = atomicAdd(&jcount[cb], 1);
                 ju[slot] = m.u; jn[slot] = m.nnn; jnu[slot] = m.nu; jal[slot] = m.alpha;
             }
             __syncthreads();
-            const int nj = jcount[i & 1];
-            if (nj > 0) {
+            PROF_MARK(1);
+            const int nj = jcount[cb];
+            cb = nb;
+            if (SELF_MIN > 0 && nj >= SELF_MIN) {
+                if (m.need) rel = ss_sca_rel_red(m.u, m.nnn, m.nu, m.alpha, err);
+            } else if (nj > 0) {
                 const int t = (int)((threadIdx.x - jrot) & (BLOCK - 1));
-                if (t < nj) __builtin_amdgcn_s_setprio(JOB_PRIO);  // the workgroup's critical path
-                for (int j = t; j < nj; j += BLOCK) {
-                    int32_t e = 0;
-                    jres[j] = ss_sca_rel_red(ju[j], jn[j], jnu[j], jal[j], e);
-                    jerr[j] = e;
+                // lanes per job (wave-uniform: nj is the workgroup's): the largest L <= GROUP_MAX_L with
+                // nj * L <= GROUP_LANES
+                const int L = (GROUP_MAX_L >= 4 && nj * 4 <= GROUP_LANES) ? 4
+                            : (GROUP_MAX_L >= 2 && nj * 2 <= GROUP_LANES) ? 2 : 1;
+                if (t < nj * L) __builtin_amdgcn_s_setprio(JOB_PRIO);  // the workgroup's critical path
+#ifdef SHYFT_PROF
+                const unsigned long long tj0 = __builtin_amdgcn_s_memtime();
+                const unsigned long long jlanes = __builtin_popcountll(__ballot(t < nj * L));
+#endif
+                if (L == 1) {
+                    for (int j = t; j < nj; j += BLOCK) {
+                        int32_t e = 0;
+                        jres[j] = ss_sca_rel_red(ju[j], jn[j], jnu[j], jal[j], e);
+                        jerr[j] = e;
+                    }
+                } else {  // a group of L consecutive lanes of one wavefront per job
+                    const int j = t / L, k = t & (L - 1);
+                    if (j < nj) {
+                        int32_t e = 0;
+                        const double r = ss_sca_rel_red_group(ju[j], jn[j], jnu[j], jal[j], L, k, e);
+                        if (k == 0) {
+                            jres[j] = r;
+                            jerr[j] = e;
+                        }
+                    }
                 }
                 __builtin_amdgcn_s_setprio(0);
+#ifdef SHYFT_PROF
+                if (jlanes && (threadIdx.x & 63) == 0) {
+                    atomicAdd(&g_ptssk_prof[8], __builtin_amdgcn_s_memtime() - tj0);
+                    atomicAdd(&g_ptssk_prof[9], 1ull);
+                    atomicAdd(&g_ptssk_prof[10], jlanes);
+                }
+#endif
+                PROF_MARK(2);
                 __syncthreads();
+                PROF_MARK(3);
                 if (slot >= 0) {
                     rel = jres[slot];
                     if (jerr[slot]) err = jerr[slot];
@@ -222,7 +300,9 @@ void ptssk_run_kernel(const ptssk_kargs a) {
             R[PR_PE_OUTPUT * RS + fo] = pot_evap;
         }
         if (SS && i + 1 == i_end) collect_state(wi + 1);
+        PROF_MARK(4);
     }
+    PROF_FLUSH();
     if (!valid) return;
     st[SS_NU * N + cell] = s.nu;
     st[SS_ALPHA * N + cell] = s.alpha;
@@ -242,11 +322,31 @@ void ptssk_run_kernel(const ptssk_kargs a) {
 #undef cell_area_m2
 #undef glacier_area_m2
 
+// r06, measured (1M cells, 730-step chunks, year mean, tools/ptgsk_variants.py): the two job functions compiled for
+// their 4-wave caller alone 85.7 ms, with this budget kernel 80.9 (the kernel saves fewer registers around the calls)
+#ifndef SHYFT_PTSSK_CALLEE_BUDGET
+#define SHYFT_PTSSK_CALLEE_BUDGET 1
+#endif
+#if SHYFT_PTSSK_CALLEE_BUDGET
+// never launched: an 8-wave caller of the job functions, so that they are register-allocated for 64 VGPRs (the
+// pt_gs_k kernel's callee-budget scheme, ptgsk.hip)
+__global__ __launch_bounds__(256, 8) void ptssk_callee_budget_kernel(const ptssk_kargs a) {
+    if (a.n_cells >= 0) return;
+    int32_t e = 0;
+    const double x = a.params[0];
+    const double r = ss_sca_rel_red((uint64_t)x, 7, x, x, e) + ss_sca_rel_red_group((uint64_t)x, 7, x, x, 2, threadIdx.x & 1, e);
+    a.resp[threadIdx.x] = r + e;
+}
+#endif
+
 }  // namespace
 
 hipError_t launch_ptssk_run(const ptssk_kargs& a, hipStream_t stream) {
     const int grid = (a.n_cells + BLOCK - 1) / BLOCK;
     if (grid == 0) return hipSuccess;
+#if SHYFT_PTSSK_CALLEE_BUDGET
+    if (a.n_cells < 0) hipLaunchKernelGGL(ptssk_callee_budget_kernel, dim3(1), dim3(BLOCK), 0, stream, a);  // never
+#endif
     if (a.uniform_params) hipLaunchKernelGGL((ptssk_run_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else hipLaunchKernelGGL((ptssk_run_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, a);
     return hipGetLastError();

@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <exception>
@@ -54,6 +55,8 @@ struct shard_set {
     unsigned flags = 0;                // SHYFT_HIP_SHARD_* options of shyft_hip_region_create_sharded_ex
     std::string report;                // how the combine path was chosen, its self-check, run-time fallbacks
     bool gather_fail_armed = false;    // SHYFT_HIP_SHARD_TEST_FAIL_GATHER: the next all-gather fails
+    bool stall_armed = false;          // SHYFT_HIP_SHARD_TEST_STALL_CHECK: the self-check's all-gather is not seen to end
+    std::string rccl_error;            // the last RCCL failure of exchange()
     size_t ens_members = 0;
     // SHYFT_HIP_SHARD_BALANCE_Z: the cells are dealt to the shards by elevation rank (fixed at the first set_geo), so
     // every shard holds the same mix of elevations; each shard keeps its cells in region order
@@ -155,6 +158,59 @@ void drop_comms(shard_set* s) {
     s->comms.clear();
 }
 
+// Every RCCL step of a region -- communicator initialisation and each all-gather -- has a deadline
+// (SHYFT_HIP_RCCL_DEADLINE_MS, default 120 s): the communicators are non-blocking (ncclConfig_t.blocking = 0), their
+// state is polled (ncclCommGetAsyncError) and the streams' completion too (hipStreamQuery), so a step that stalls
+// fails like one that errs -- the communicators are aborted and the region continues on device copies.
+using clock_t_ = std::chrono::steady_clock;
+long long rccl_deadline_ms() {
+    const char* e = getenv("SHYFT_HIP_RCCL_DEADLINE_MS");  // read at every step: a test may change it
+    const long long ms = e ? atoll(e) : 0;
+    return ms > 0 ? ms : 120000;
+}
+
+clock_t_::time_point rccl_deadline() { return clock_t_::now() + std::chrono::milliseconds(rccl_deadline_ms()); }
+
+std::string deadline_text() { return std::to_string(rccl_deadline_ms()) + " ms"; }
+
+// a non-blocking RCCL call: ncclInProgress is the normal answer
+void nccl_nb(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess && r != ncclInProgress) nccl_check(r, what);
+}
+
+// wait until no communicator is ncclInProgress; throws on an error state or at the deadline
+void wait_comms(shard_set* s, const char* what, clock_t_::time_point until) {
+    for (;;) {
+        bool pending = false;
+        for (ncclComm_t c : s->comms) {
+            ncclResult_t st = ncclSuccess;
+            nccl_check(ncclCommGetAsyncError(c, &st), "ncclCommGetAsyncError");
+            if (st == ncclInProgress) pending = true;
+            else nccl_check(st, what);
+        }
+        if (!pending) return;
+        if (clock_t_::now() > until)
+            throw std::runtime_error(std::string(what) + " did not complete within " + deadline_text());
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// wait for the shards' streams; throws on an error or at the deadline. stall: the test of a stalled collective
+// (SHYFT_HIP_SHARD_TEST_STALL_CHECK) -- the work has completed, but the wait behaves as if it had not
+bool wait_streams(shard_set* s, clock_t_::time_point until, bool stall = false) {
+    for (size_t k = 0; k < s->S(); ++k) {
+        hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+        for (;;) {
+            const hipError_t q = stall ? hipErrorNotReady : hipStreamQuery(s->streams[k]);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) hip_check(q, "ncclAllGather completion");
+            if (clock_t_::now() > until) return false;
+            std::this_thread::sleep_for(std::chrono::microseconds(stall ? 2000 : 20));
+        }
+    }
+    return true;
+}
+
 // the all-gather step of combine(): bufs[k]->full [M] of every shard -> [S][M] partials on shard 0's device in
 // bufs[0]->gath (RCCL: on every shard's device). An RCCL failure at run time (an error status from the group) drops
 // the communicators and switches the region to device copies for this and every later combine: the reference's
@@ -162,31 +218,37 @@ void drop_comms(shard_set* s) {
 void exchange(shard_set* s, size_t M) {
     const size_t S = s->S();
     if (s->path == SHYFT_HIP_COMBINE_RCCL) {
+        bool group_open = false;
         try {
             if (s->gather_fail_armed) {
                 s->gather_fail_armed = false;
                 throw std::runtime_error("ncclAllGather: injected failure (SHYFT_HIP_SHARD_TEST_FAIL_GATHER)");
             }
+            const clock_t_::time_point until = rccl_deadline();
             nccl_check(ncclGroupStart(), "ncclGroupStart");
+            group_open = true;
             for (size_t k = 0; k < S; ++k) {
                 hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
-                nccl_check(ncclAllGather(s->bufs[k]->full.p, s->bufs[k]->gath.p, M, ncclDouble, s->comms[k], s->streams[k]),
-                           "ncclAllGather");
+                nccl_nb(ncclAllGather(s->bufs[k]->full.p, s->bufs[k]->gath.p, M, ncclDouble, s->comms[k], s->streams[k]),
+                        "ncclAllGather");
             }
-            nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-            for (size_t k = 0; k < S; ++k) {
-                hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
-                hip_check(hipStreamSynchronize(s->streams[k]), "ncclAllGather completion");
-            }
+            group_open = false;
+            nccl_nb(ncclGroupEnd(), "ncclGroupEnd");
+            wait_comms(s, "ncclAllGather", until);
+            const bool stall = s->stall_armed;
+            s->stall_armed = false;
+            if (!wait_streams(s, until, stall))
+                throw std::runtime_error("ncclAllGather did not complete within " + deadline_text() +
+                                         (stall ? " (injected stall, SHYFT_HIP_SHARD_TEST_STALL_CHECK)" : ""));
             hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
             return;
         } catch (const std::exception& e) {
-            for (size_t k = 0; k < S; ++k) {
-                (void)hipSetDevice(s->dev[k]);
-                (void)hipStreamSynchronize(s->streams[k]);
-            }
-            drop_comms(s);
+            // a group left open would defer this thread's next RCCL calls: close it first
+            if (group_open) (void)ncclGroupEnd();
+            drop_comms(s);  // ncclCommAbort: pending RCCL work of the region ends
+            (void)wait_streams(s, rccl_deadline());
             s->path = SHYFT_HIP_COMBINE_COPY;
+            s->rccl_error = e.what();
             s->report += std::string("; RCCL failed at run time (") + e.what() + "): device copies from then on";
         }
     }
@@ -221,7 +283,7 @@ std::string rccl_self_check(shard_set* s) {
             hip_check(hipStreamSynchronize(s->streams[k]), "self-check upload");
         }
         exchange(s, M);
-        if (s->path != SHYFT_HIP_COMBINE_RCCL) return "the all-gather failed";
+        if (s->path != SHYFT_HIP_COMBINE_RCCL) return "the all-gather failed: " + s->rccl_error;
         std::vector<double> got(S * M);
         for (size_t k = 0; k < S; ++k) {
             hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
@@ -279,14 +341,35 @@ void choose_path(shard_set* s) {
     try {
         if (s->flags & SHYFT_HIP_SHARD_TEST_FAIL_INIT)
             throw std::runtime_error("ncclCommInitAll: injected failure (SHYFT_HIP_SHARD_TEST_FAIL_INIT)");
+        // one non-blocking communicator per device, created in one group (ncclCommInitAll's communicators, with a
+        // deadline on their initialisation)
+        const clock_t_::time_point until = rccl_deadline();
+        ncclUniqueId id;
+        nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
         s->comms.assign(S, nullptr);
-        nccl_check(ncclCommInitAll(s->comms.data(), int(S), s->dev.data()), "ncclCommInitAll");
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        try {
+            for (size_t k = 0; k < S; ++k) {
+                hip_check(hipSetDevice(s->dev[k]), "hipSetDevice");
+                ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+                cfg.blocking = 0;
+                nccl_nb(ncclCommInitRankConfig(&s->comms[k], int(S), id, int(k), &cfg), "ncclCommInitRankConfig");
+            }
+        } catch (...) {
+            (void)ncclGroupEnd();
+            throw;
+        }
+        nccl_nb(ncclGroupEnd(), "ncclGroupEnd");
+        wait_comms(s, "RCCL communicator initialisation", until);
+        hip_check(hipSetDevice(s->dev[0]), "hipSetDevice");
     } catch (const std::exception& e) {
         drop_comms(s);
+        (void)hipSetDevice(s->dev[0]);
         s->report = std::string("copy: RCCL initialisation failed (") + e.what() + "), device copies instead";
         return;
     }
     s->path = SHYFT_HIP_COMBINE_RCCL;
+    s->stall_armed = (s->flags & SHYFT_HIP_SHARD_TEST_STALL_CHECK) != 0;
     const std::string bad = rccl_self_check(s);
     if (!bad.empty()) {
         drop_comms(s);
@@ -294,7 +377,7 @@ void choose_path(shard_set* s) {
         s->report = "copy: RCCL self-check failed (" + bad + "), device copies instead";
         return;
     }
-    s->report = "rccl: ncclCommInitAll over devices " + devs + "; self-check passed (all-gather of " +
+    s->report = "rccl: non-blocking communicators over devices " + devs + "; self-check passed (all-gather of " +
                 std::to_string(S) + " x 4096 known doubles bit-exact on every device, shard-order sums bit-equal to "
                 "the device-copy path)";
     s->gather_fail_armed = (s->flags & SHYFT_HIP_SHARD_TEST_FAIL_GATHER) != 0;
@@ -487,6 +570,14 @@ void deal_by_elevation(shard_set* s, const double* geo11) {
     for_shards(s, [&](size_t k) { region_set_cell_ids(s->r[k], s->cells[k].data()); });
 }
 
+// SHYFT_HIP_SHARD_BALANCE_Z deals the cells at the first set_geo; per-cell data given before that would be split
+// by contiguous ranges and then belong to the wrong cells, so it is refused
+void require_dealt(const shard_set* s, const char* what) {
+    if ((s->flags & SHYFT_HIP_SHARD_BALANCE_Z) && !s->permuted)
+        throw std::runtime_error(std::string(what) + ": a region whose shards are dealt by elevation "
+                                 "(SHYFT_HIP_SHARD_BALANCE_Z) takes per-cell data only after its first set_geo");
+}
+
 void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double* rdist) {
     // the deal is fixed by the first geometry (later set_geo calls keep it: a layout, not a result)
     if ((s->flags & SHYFT_HIP_SHARD_BALANCE_Z) && !s->permuted) deal_by_elevation(s, geo11);
@@ -501,6 +592,7 @@ void set_geo(shard_set* s, const double* geo11, const int64_t* rid, const double
 }
 
 void set_parameters(shard_set* s, const double* params, size_t n_sets, size_t n_per_set, const int32_t* set_ix) {
+    if (set_ix) require_dealt(s, "set_parameters (per-cell set index)");
     for_shards(s, [&](size_t k) {
         std::vector<int32_t> ix;
         ck(s->r[k], shyft_hip_set_parameters(s->r[k], params, n_sets, n_per_set, shard_rows(s, k, set_ix, 1, ix)));
@@ -543,6 +635,7 @@ void set_catchment_filter(shard_set* s, const int64_t* cids, size_t n) {
 }
 
 void set_state(shard_set* s, const double* state, size_t n_fields) {
+    require_dealt(s, "set_state");
     for_shards(s, [&](size_t k) {
         std::vector<double> rows;
         ck(s->r[k], shyft_hip_set_state(s->r[k], shard_rows(s, k, state, n_fields, rows), n_fields));
@@ -550,6 +643,7 @@ void set_state(shard_set* s, const double* state, size_t n_fields) {
 }
 
 void get_state(shard_set* s, double* state, size_t n_fields) {
+    require_dealt(s, "get_state");
     for_shards(s, [&](size_t k) {
         if (!s->permuted) {
             ck(s->r[k], shyft_hip_get_state(s->r[k], state + s->b[k] * n_fields, n_fields));
@@ -571,6 +665,7 @@ void copy_state(shard_set* d, const shard_set* src) {
 
 void set_forcing(shard_set* s, int var, size_t step0, size_t n, const double* src, int on_device) {
     if (on_device) throw std::runtime_error("set_forcing: a sharded region takes forcing from host memory");
+    require_dealt(s, "set_forcing");
     for_shards(s, [&](size_t k) {
         std::vector<double> blk;
         split_cols(s, src, n, k, blk);
@@ -622,6 +717,7 @@ void interpolate_btk(shard_set* s, size_t n_sources, const double* xyz, const do
 }
 
 void synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t step0, size_t n) {
+    require_dealt(s, "synthetic_forcing");
     for_shards(s, [&](size_t k) {
         // generator cell of shard cell j: cell_offset + its region cell (contiguous: b[k] + j; dealt: the shard's
         // cell ids, region_set_cell_ids)
@@ -630,6 +726,7 @@ void synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t
 }
 
 void prefetch_synthetic_forcing(shard_set* s, uint64_t seed, uint64_t cell_offset, size_t w0_next, int n_cus) {
+    require_dealt(s, "prefetch_synthetic_forcing");
     for_shards(s, [&](size_t k) {
         ck(s->r[k], shyft_hip_prefetch_synthetic_forcing(s->r[k], seed, cell_offset + (s->permuted ? 0 : s->b[k]),
                                                          w0_next, n_cus));
@@ -795,6 +892,7 @@ void catchment_ids(const shard_set* s, int64_t* cids) {
 }
 
 void set_routing_groups(shard_set* s, const int32_t* group_of_cell, size_t n_groups) {
+    require_dealt(s, "set_routing_groups");
     for_shards(s, [&](size_t k) {
         std::vector<int32_t> g;
         ck(s->r[k], shyft_hip_set_routing_groups(s->r[k], shard_rows(s, k, group_of_cell, 1, g), n_groups));

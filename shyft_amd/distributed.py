@@ -57,8 +57,9 @@ def verify_collectives(device=None, group=None, inject_failure: bool = False, m:
     contributes m known doubles, every rank must receive all of them bit for bit. The ranks agree on the outcome
     over the host backend (a CPU all-reduce of a flag); if any rank failed (or the collective raised), every later
     combine_partials / max_over_ranks moves its partials through the host backend instead -- the same values,
-    slower. With a mixed process group ("cpu:gloo,cuda:nccl") that host path needs no second group. Returns the
-    report (also in combine_report()). inject_failure: the fallback test's failure on this rank."""
+    slower. With a mixed process group ("cpu:gloo,cuda:nccl") that host path needs no second group; a group with no
+    host backend (RCCL alone) has no such path, and a failed self-check raises there instead. Returns the report
+    (also in combine_report()). inject_failure: the fallback test's failure on this rank."""
     import torch
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
@@ -66,15 +67,22 @@ def verify_collectives(device=None, group=None, inject_failure: bool = False, m:
         return _COMBINE["report"]
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     ok, why = True, ""
+    # the tensors are built before the collective, and every rank enters the all-gather exactly once whatever fails
+    # on it (a rank that skipped it would leave the others blocked in it)
     try:
         t = _known(rank, m)
         if device is not None:
             t = t.to(device)
         parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t, group=group)   # every rank enters the collective, failing or not
+    except Exception as e:  # noqa: BLE001 -- preparation failed: take part with a dummy, report the failure
+        ok, why = False, f"{type(e).__name__}: {e}"
+        t = torch.zeros(m, dtype=torch.float64, device=device if device is not None else "cpu")
+        parts = [torch.empty_like(t) for _ in range(world)]
+    try:
+        dist.all_gather(parts, t, group=group)
         if inject_failure:
             raise RuntimeError("injected all-gather failure")
-        for r in range(world):
+        for r in range(world) if ok else ():
             got = parts[r].cpu().view(torch.int64)
             if not torch.equal(got, _known(r, m).view(torch.int64)):
                 ok, why = False, f"rank {rank} received rank {r}'s values with different bits"
@@ -82,7 +90,8 @@ def verify_collectives(device=None, group=None, inject_failure: bool = False, m:
     except Exception as e:  # noqa: BLE001 -- any failure of the device path means: use the host path
         ok, why = False, f"{type(e).__name__}: {e}"
     flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
-    if "gloo" in str(dist.get_backend(group)) or device is None:
+    host_backend = "gloo" in str(dist.get_backend(group)) or device is None
+    if host_backend:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)   # host tensor: the group's CPU backend
     else:  # a device-only group: agree over the device (no host path to fall back to then)
         fd = flag.to(device)
@@ -93,8 +102,12 @@ def verify_collectives(device=None, group=None, inject_failure: bool = False, m:
         _COMBINE.update(host=False, report=f"{kind} all-gather self-check passed ({world} ranks x {m} known doubles "
                                            f"bit-exact on every rank)")
     else:
-        _COMBINE.update(host=True, report="host (gloo) combines: the device all-gather self-check failed"
-                                          + (f" on this rank ({why})" if why else " on another rank"))
+        report = ("the device all-gather self-check failed" + (f" on this rank ({why})" if why else " on another rank"))
+        if not host_backend:
+            # a group without a CPU backend cannot move host tensors: no combine could work, say so now
+            _COMBINE.update(host=False, report=report + "; no host backend in this process group")
+            raise RuntimeError(_COMBINE["report"])
+        _COMBINE.update(host=True, report="host (gloo) combines: " + report)
     return _COMBINE["report"]
 
 

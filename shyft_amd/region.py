@@ -31,6 +31,7 @@ KNOB_PTGSK_INSTANCE, KNOB_BRENT_READ_DELAY, KNOB_SERIAL_SHARDS, KNOB_CLONE_FAIL_
 # shyft_hip_region_create_sharded_ex options (include/shyft_hip.h)
 SHARD_RCCL_ALWAYS, SHARD_NO_RCCL, SHARD_TEST_FAIL_INIT, SHARD_TEST_FAIL_GATHER, SHARD_TEST_CORRUPT_CHECK = 1, 2, 4, 8, 16
 SHARD_BALANCE_Z = 32
+SHARD_TEST_STALL_CHECK = 64
 # pt_ss_k (core/pt_ss_k.h:154-181, pt_ss_k_cell_model.h:38-200); response series ids are the pt_gs_k ones
 PTSSK_STATE = ("nu", "alpha", "sca", "swe", "free_water", "residual", "num_units", "kirchner_q")
 PTSSK_STATE_SERIES = ("kirchner_discharge", "snow_sca", "snow_swe", "snow_alpha", "snow_nu", "snow_lwc",

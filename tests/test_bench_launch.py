@@ -42,6 +42,31 @@ def test_launcher_gloo_dist_check(world, cells, catch):
     assert out["max_abs_diff"] < 1e-9
 
 
+@pytest.mark.parametrize("stalled", [1, 0])
+def test_stalled_self_check_restarts_ranks_with_host_combines(stalled):
+    """One rank stalls inside the collective self-check of the first attempt (SHYFT_DIST_TEST_STALL): its supervisor
+    sees no progress within the stall limit, every rank's child is killed and replaced by a fresh one (no process that
+    ran is re-executed), and the second attempt -- gloo combines -- prints the line, saying why the first ended."""
+    t0 = __import__("time").monotonic()
+    p, out = _bench(["--gpus", "2", "--dist-check", "--total-cells", "4096"],
+                    env_extra={"SHYFT_DIST_TEST_STALL": f"{stalled}:0", "SHYFT_SUPERVISE_STALL_S": "6",
+                               "SHYFT_SUPERVISE_FIRST_S": "120", "SHYFT_DIST_TIMEOUT_S": "60"}, timeout=240)
+    took = __import__("time").monotonic() - t0
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert out is not None and out["max_abs_diff"] < 1e-9
+    sup = out["supervisor"]
+    assert sup["attempt"] == 1 and sup["combines"] == "gloo"
+    assert "made no progress" in sup["previous_attempt"] or "exited with status" in sup["previous_attempt"]
+    assert took < 120, took   # the stall limit (6 s) and two start-ups, far below the collective timeout (60 s)
+    assert len([l for l in p.stdout.splitlines() if l.startswith("{")]) == 1
+
+
+def test_first_attempt_line_carries_supervisor_field():
+    p, out = _bench(["--gpus", "2", "--dist-check", "--total-cells", "4096"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["supervisor"]["attempt"] == 0 and out["supervisor"]["previous_attempt"] is None
+
+
 def test_world_size_mismatch_fails():
     p, out = _bench(["--gpus", "2", "--dist-check"], env_extra={"WORLD_SIZE": "3", "RANK": "0"})
     assert p.returncode != 0 and out is None

@@ -106,7 +106,7 @@ def test_ptssk_ragged_parameter_sets_and_stepwise():
 @pytest.mark.gpu
 def test_ptssk_odd_start_step_and_single_steps_in_melt():
     """run_cells from an ODD start_step and one step at a time in April (partial melts queue sca_rel_red
-    jobs): the double-buffered job counter starts at zero for either parity of the first step."""
+    jobs): the rotating job counters start at zero whatever the first step."""
     n, T = 300, 24 * 4
     step0 = 24 * 100
     geo, f = _case(n, T, step0=step0, seed=11)
@@ -137,3 +137,21 @@ def test_ptssk_odd_start_step_and_single_steps_in_melt():
         assert np.array_equal(r.get_state(), ref["state"])
     finally:
         r.close()
+
+
+@pytest.mark.gpu
+def test_ptssk_year_every_job_group_size_bitexact():
+    """A whole year (spring and autumn melts) of 2048 cells: steps with a few sca_rel_red jobs per workgroup give each
+    job a group of 4 or 2 lanes (grouped lgammas, opening evaluations, cdfs, and 2 bisection levels per round), busy
+    steps one lane per job, and the bisection takes its midpoints' signs without the pdf divisions where they are
+    certain (device/ptssk_dev.h). Every series and the end state must equal the oracle's."""
+    n, T = 2048, 8760
+    geo, f = _case(n, T, seed=13)
+    st = synthetic.default_ptssk_state(n)
+    p = synthetic.default_ptssk_parameters()
+    ref = engines.run_ptssk("oracle", geo, p, st, synthetic.T0_2015_US, HOUR, f)
+    got = engines.run_ptssk("hip", geo, p, st, synthetic.T0_2015_US, HOUR, f)
+    _assert_same(ref, got, ("full", "state"))
+    swe = ref["full"][3]
+    autumn = slice(24 * 243, 24 * 334)   # Sep - Nov: few partial melts per step
+    assert (swe[autumn] > 0).any() and (swe[:24 * 150] > 0).any()

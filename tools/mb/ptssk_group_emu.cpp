@@ -1,0 +1,104 @@
+// Analysis (CPU): the pt_ss_k job solver's two rewrites of the bisection (device/ptssk_dev.h ss_sca_rel_red_body),
+// replayed against the oracle's boost::math::tools::bisect restatement (oracle/src/ptssk.hpp) on recorded jobs:
+//  1. the grouped rounds: the midpoints of the next D levels evaluated at once (D = 2: groups of 4 lanes; D = 3: 8),
+//     then the sequential loop replayed over them;
+//  2. ss_zero_sign: the midpoint's sign without the pdfs' divisions where it is certain.
+// Both must end on the oracle's bracket, bit for bit, for every job.
+// jobs: tools/mb/ptssk_jobs -o jobs.bin (u, n, nu_a, alpha, ... per row of 9 doubles)
+// build: g++ -O2 -std=c++17 -mfma -ffp-contract=off -o tools/mb/ptssk_group_emu tools/mb/ptssk_group_emu.cpp
+#include <cstdio>
+#include <vector>
+
+#include "../../oracle/src/ptssk.hpp"
+
+using namespace oracle;
+
+int main(int argc, char** argv) {
+    if (argc < 2) { fprintf(stderr, "usage: ptssk_group_emu jobs.bin\n"); return 2; }
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    std::vector<double> J;
+    double row[9];
+    while (fread(row, sizeof(double), 9, f) == 9) J.insert(J.end(), row, row + 9);
+    fclose(f);
+    const size_t nr = J.size() / 9;
+    long bad_group[4] = {0}, bad_sign = 0, fast = 0, slow = 0, checked = 0;
+    for (size_t r = 0; r < nr; ++r) {
+        const double* q = &J[9 * r];
+        const unsigned long u = (unsigned long)q[0], n = (unsigned long)q[1];
+        const double nu_a = q[2], alpha = q[3];
+        const double nu_m = ((double)u / n) * nu_a, theta = 1.0 / alpha;
+        const skaugen::gamma_dist g_m{nu_m, theta}, g_a{nu_a, theta};
+        const double lg_m = OLGAMMA(nu_m), lg_a = OLGAMMA(nu_a);
+        auto zf = [&](double x) { return g_m.pdf(x) - g_a.pdf(x); };
+        auto zs = [&](double x) {  // ss_zero_sign (x > 0 here)
+            const double z = x / theta, lz = OLOG(z);
+            const double ea = OEXP(nu_m * lz - z - lg_m), eb = OEXP(nu_a * lz - z - lg_a);
+            if (ea == 0 && eb == 0) { ++fast; return 0.0; }
+            const double LO = 0x1p-960, HI = 0x1p960;
+            if (z >= 0x1p-30 && z <= 0x1p30 && theta >= 0x1p-30 && theta <= 0x1p30) {
+                if (eb >= LO && eb <= HI && eb > ea * (1.0 + 0x1p-48)) { ++fast; return -1.0; }
+                if (ea >= LO && ea <= HI && ea > eb * (1.0 + 0x1p-48)) { ++fast; return 1.0; }
+            }
+            ++slow;
+            return ea / z / theta - eb / z / theta;
+        };
+        double lower = g_m.mean();
+        uintmax_t bi = ~0ull;
+        const double upper = special::brent_find_minima(zf, 0.0, g_a.mean(), 2, bi).first;
+        while (g_m.pdf(lower) < g_a.pdf(lower)) lower *= 0.9;
+        uintmax_t mi = 100;
+        const auto ref = skaugen::bisect(zf, lower, upper, 10, mi);
+        const double fmin0 = zf(lower), fmax0 = zf(upper);
+        if (fmin0 == 0 || fmax0 == 0 || lower >= upper || fmin0 * fmax0 >= 0) continue;
+        ++checked;
+        const double eps = 0x1p-9;
+        auto sgn = [](double v) { return v > 0 ? 1 : (v < 0 ? -1 : 0); };
+        for (int mode = 0; mode < 3; ++mode) {  // 0: sign surrogate, sequential; 1: D = 2; 2: D = 3
+            double bmin = lower, bmax = upper, fmin = fmin0;
+            int count = 97;
+            auto go_on = [&]() { return count && !(std::fabs(bmin - bmax) <= eps * std::min(std::fabs(bmin), std::fabs(bmax))); };
+            if (mode == 0) {
+                while (go_on()) {
+                    const double mid = (bmin + bmax) / 2, fmid = zs(mid);
+                    if (mid == bmax || mid == bmin) break;
+                    if (fmid == 0) { bmin = bmax = mid; break; }
+                    if (sgn(fmid) * sgn(fmin) < 0) bmax = mid; else { bmin = mid; fmin = fmid; }
+                    --count;
+                }
+                if (bmin != ref.first || bmax != ref.second) ++bad_sign;
+                continue;
+            }
+            const int D = mode + 1, P = (1 << D) - 1;
+            bool more = go_on();
+            while (more) {
+                double fk[8];
+                for (int k = 0; k < P; ++k) {  // lane k's point: heap node k + 1
+                    const int h = k + 1, depth = 31 - __builtin_clz((unsigned)h);
+                    double lo = bmin, hi = bmax;
+                    for (int b = depth - 1; b >= 0; --b) {
+                        const double m2 = (lo + hi) / 2;
+                        if ((h >> b) & 1) lo = m2; else hi = m2;
+                    }
+                    fk[k] = zs((lo + hi) / 2);
+                }
+                int node = 1;
+                for (int lev = 0; lev < D; ++lev) {
+                    if (lev > 0 && !go_on()) { more = false; break; }
+                    const double mid = (bmin + bmax) / 2, fmid = fk[node - 1];
+                    if (mid == bmax || mid == bmin) { more = false; break; }
+                    if (fmid == 0) { bmin = bmax = mid; more = false; break; }
+                    if (sgn(fmid) * sgn(fmin) < 0) { bmax = mid; node = 2 * node; }
+                    else { bmin = mid; fmin = fmid; node = 2 * node + 1; }
+                    --count;
+                }
+                if (more) more = go_on();
+            }
+            if (bmin != ref.first || bmax != ref.second) ++bad_group[D];
+        }
+    }
+    printf("jobs %zu, bisections checked %ld: differing brackets: sign surrogate %ld, D=2 %ld, D=3 %ld; "
+           "surrogate evaluations without the divisions %ld, with %ld\n",
+           nr, checked, bad_sign, bad_group[2], bad_group[3], fast, slow);
+    return (bad_sign || bad_group[2] || bad_group[3]) ? 1 : 0;
+}

@@ -60,6 +60,7 @@ print(json.dumps({"ms": ms, "digest": h.hexdigest()[:16] + "/" + h0}))
 def main():
     args = sys.argv[1:]
     cells, chunks, stack = 1 << 20, 12, "pt_gs_k"
+    args = [x for x in args if x != "--keep-going"]
     while args and args[0].startswith("--"):
         k, v = args[0], args[1]
         args = args[2:]
@@ -80,6 +81,8 @@ def main():
             d = json.loads(out.stdout.strip().splitlines()[-1])
         except Exception:
             print(spec, "FAILED", out.stderr[-1500:], flush=True)
+            if "--keep-going" not in sys.argv:
+                sys.exit(1)  # a fault leaves the GPU in an unknown state: run nothing more
             continue
         if ref is None:
             ref = d["digest"]
