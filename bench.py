@@ -153,6 +153,17 @@ IDW_DEFAULTS = {
 }
 
 
+def idw_gather_bytes(var, cells, rows, n_sources=N_STATIONS):
+    """Algorithmic HBM bytes of one IDW gather launch (kernels/idw.hip, wavefront-union path) for forcing variable
+    `var` over `rows` steps: the window rows it writes (8 B per cell-step) plus what it reads once per launch -- per
+    cell the neighbour table (K packed 1-byte local indexes, K weights, and for temperature / precipitation K
+    transform terms: d.z - s.z or pow(scale, dz/100)), its member count, the cell's z (temperature) or slope
+    (radiation), its wavefront's share of the union list (64 x 4 B per 64 cells), and the [rows][sources] values."""
+    K = int(IDW_DEFAULTS[var][0])
+    per_cell = K * (1 + 8 + (8 if var in (0, 1) else 0)) + 4 + 4 + (8 if var in (0, 4) else 0)
+    return cells * rows * 8 + cells * per_cell + rows * n_sources * 8
+
+
 # bayesian_kriging::parameter() defaults (bayesian_kriging.h:204-217) in the C ABI layout:
 # gradient_sd [C/m], sill, nugget, range, zscale
 BTK_DEFAULTS = [0.0025, 25.0, 0.5, 200000.0, 20.0]
@@ -408,7 +419,7 @@ class CatchmentSums:
 
 
 def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, btk_ms=None,
-             r_alt=None, sums=None, walls=None, parts=None, overlap=0):
+             r_alt=None, sums=None, walls=None, parts=None, overlap=0, idw_ms=None):
     """K bench steps from Jan 1: per chunk put the chunk's forcing into HBM (device generator,
     or IDW / BTK from the station network), then run_cells (and the routing group sums).
 
@@ -433,6 +444,7 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
         else:
             xyz, vals = stations
             v = vals[s % len(vals)]
+            gms = [0.0] * 5
             for var in range(5):
                 if var == 0 and btk:
                     t = time.perf_counter()
@@ -441,6 +453,9 @@ def run_year(r, L, chunk, k_steps, seed, stations=None, router=None, btk=False, 
                         btk_ms.append((time.perf_counter() - t) * 1e3)
                 else:
                     r.interpolate(var, xyz, v[var], step0, IDW_DEFAULTS[var])
+                    gms[var] = r.last_interpolate_ms()   # the gather kernel alone (HIP events)
+            if idw_ms is not None:
+                idw_ms.append(gms)
         r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
         if parts is not None:
@@ -555,7 +570,40 @@ def cpu_baseline(stack, n_cells, threads):
     }
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+def cpu_baseline_idw(n_cells, threads):
+    """configs[2] on the CPU: the oracle's inverse-distance interpolation (oracle/src/idw.hpp, restating
+    core/inverse_distance.h:142-250; host libm) of the five variables from the same 500-station network onto the first
+    n_cells cells of the 1M-cell region, then the pt_gs_k oracle with the reference scheduler, over the year."""
+    from shyft_amd import synthetic
+    from tests import oracle_lib
+    xyz = station_network(1 << 20)
+    vals = station_values(xyz, 0, YEAR)                      # [5][YEAR][S], prepared before timing (an input)
+    geo = synthetic.geo11(n_cells, n_total=1 << 20)
+    dst = np.ascontiguousarray(geo[:, 0:3])
+    kinds = (0, 1, 3, 4, 2)                                  # oracle kinds of T, P, WS, RH, RAD
+    t0 = time.perf_counter()
+    f = np.stack([oracle_lib.idw_run(kinds[v], xyz, vals[v], dst, IDW_DEFAULTS[v],
+                                     dst_slope=geo[:, 5] if v == 4 else None, variant="libm") for v in range(5)])
+    t_idw = time.perf_counter() - t0
+    p, st = stack_defaults("pt_gs_k", n_cells)
+    res = oracle_lib.ptgsk_run(geo, p, st, synthetic.T0_2015_US, synthetic.HOUR_US, f, ncore=threads, variant="libm")
+    el = t_idw + res["elapsed_s"]
+    return {
+        "value": n_cells * YEAR / el,
+        "unit": "cell-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n_cells} cells x {YEAR} hourly steps of the configs[2] region (first cells of the 1M-cell region, "
+                  f"{N_STATIONS} stations): oracle IDW of the 5 variables (host libm, destinations split over up to 16 "
+                  f"threads: {t_idw:.2f} s) + pt_gs_k oracle with the reference scheduler, use_ncore={threads} "
+                  f"({res['elapsed_s']:.2f} s)",
+        "idw_s": t_idw,
+        "run_cells_s": res["elapsed_s"],
+        "cpu_model": _cpu_model(),
+    }
+
+
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")
 
 
 def workload_tag(a, cells):
@@ -564,13 +612,13 @@ def workload_tag(a, cells):
             f"_s{a.steps}_w{a.warmup}{f'_sh{a.shards}' if a.shards > 1 else ''}")
 
 
-def pmc_summary(a, cells):
+def pmc_summary(a, cells, suffix=""):
     """(summary, reason): the committed rocprofv3 PMC summary of the dominant kernel
     (profiles/<round>/pmc_<workload>.json, written by tools/gpu_profile.sh + tools/pmc_summary.py from this same
     bench command) -- only if it measured THIS build of the library (same sha256), else (None, why). PMC counters
     cannot be read from inside this process."""
     from shyft_amd import _native
-    rel = f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json"
+    rel = f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}{suffix}.json"
     try:
         d = json.load(open(os.path.join(ROOT, rel)))
     except (OSError, ValueError):
@@ -696,8 +744,9 @@ def main():
     t0 = time.perf_counter()
     btk_ms = []
     walls, parts = [], []
+    idw_ms = []
     kernel_ms = run_year(r, L, chunk, a.steps, synthetic.SEED, stations, router, a.btk, btk_ms,
-                         r_alt=r_alt, sums=sums, walls=walls, parts=parts, overlap=a.overlap_forcing)
+                         r_alt=r_alt, sums=sums, walls=walls, parts=parts, overlap=a.overlap_forcing, idw_ms=idw_ms)
     barrier_sync(pg, local, devices)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(pg, local, wall)
@@ -789,7 +838,10 @@ def main():
         ny = YEAR // chunk
         out["calendar_year"] = {
             "value": L.total * chunk * ny / (sum(walls[:ny]) * 1e-3), "unit": "cell-steps/s",
-            "chunks": f"timed chunks 1-{ny} (Jan 1 - Dec 31, {YEAR} hourly steps: BASELINE configs[1]'s year)",
+            "chunks": f"timed chunks 1-{ny} (Jan 1 - Dec 31, {YEAR} hourly steps: " + {
+                "pt_gs_k": "BASELINE configs[2]'s year" if a.idw else "BASELINE configs[1]'s year",
+                "hbv_stack": "BASELINE configs[3]'s year", "pt_ss_k": "the first year of BASELINE configs[4]'s 3-year "
+                "horizon"}.get(a.stack, "one calendar year") + ")",
             "ms_per_step": sum(walls[:ny]) / ny,
             "kernel_ms_per_step": float(np.mean(kernel_ms[:ny])),
             "note": "per-chunk wall clocks of this same timed run (synchronised at the end of each chunk)"}
@@ -806,6 +858,35 @@ def main():
                          "write_GBps": cells * chunk * 8 / (ms * 1e-3) / 1e9,
                          "note": "2 * cells * (stations + 3) * chunk flops per call over its wall time "
                                  "(host part included)"},
+        }
+    if a.idw and not a.btk and idw_ms:
+        # configs[2]'s interpolation: the five IDW gathers of every chunk (kernels/idw.hip), HBM-bound accounting as
+        # the run kernel's, over the gathers' own HIP-event times
+        per_var = [float(max_over_ranks(pg, local, float(np.mean([c[v] for c in idw_ms])))) for v in range(5)]
+        b_var = [idw_gather_bytes(v, cells, chunk) for v in range(5)]
+        ms_chunk = float(sum(per_var))
+        ipmc, ipmc_missing = pmc_summary(a, cells, suffix="_idw_gather")
+        itraffic = None if ipmc is None else ipmc["traffic_bytes_per_launch_sum"]
+        out["idw"] = {
+            "kernel_ms_per_chunk": ms_chunk,
+            "share_of_chunk_wall": ms_chunk / (wall * 1e3 / a.steps),
+            "by_variable_ms": dict(zip(("temperature", "precipitation", "wind_speed", "rel_hum", "radiation"),
+                                       [round(x, 3) for x in per_var])),
+            "roofline": {
+                "bound": "hbm", "achieved": sum(b_var) / (ms_chunk * 1e-3) / 1e9, "peak": HBM_PEAK_BPS / 1e9,
+                "unit": "GB/s", "frac": sum(b_var) / (ms_chunk * 1e-3) / HBM_PEAK_BPS,
+                "temperature_GBps": b_var[0] / (per_var[0] * 1e-3) / 1e9,
+                "traffic": None if itraffic is None else itraffic / (ms_chunk * 1e-3) / 1e9,
+                "traffic_bytes_per_chunk": itraffic,
+                "traffic_source": ipmc_missing if ipmc is None else
+                f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}_idw_gather.json (library "
+                f"sha256 {ipmc['lib_sha256'][:16]}, the one this run loaded): the five gathers' FETCH_SIZE x "
+                f"{ipmc['calibration']['fetch_correction']:.3f} + WRITE_SIZE per chunk, mean over the timed chunks",
+                "valu_busy": None if ipmc is None else ipmc["valu_busy"],
+                "algorithmic_bytes_per_chunk": sum(b_var),
+                "kernel": "idw_wave_gather_kernel (5 launches per chunk, one per forcing variable)",
+                "note": "algorithmic bytes: 8 B written per cell-step + the neighbour tables and source rows read "
+                        "once per launch (bench.idw_gather_bytes)"},
         }
     if pmc is not None:
         # the bound that does apply to the VALU-bound stacks: fp64 VALU issue. SQ_ACTIVE_INST_VALU (quad-cycles of
@@ -847,7 +928,8 @@ def main():
         out["supervisor"] = supervisor_info()
     if rank == 0 and world == 1 and not devices and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        out["cpu_baseline"] = cpu_baseline(a.stack, a.cpu_cells, threads)
+        out["cpu_baseline"] = (cpu_baseline_idw(a.cpu_cells, threads) if a.idw and not a.btk and a.stack == "pt_gs_k"
+                               else cpu_baseline(a.stack, a.cpu_cells, threads))
     if rank == 0:
         print(json.dumps(out), flush=True)
     r.close()

@@ -234,6 +234,10 @@ double shyft_hip_last_run_ms(const shyft_hip_region* h);
    a sharded region: the slowest running shard's). Fills ms[0..min(n, parts)) and returns the number of parts.
    (No reference counterpart: measurement only.) */
 int shyft_hip_last_run_kernel_ms(const shyft_hip_region* h, double* ms, int n);
+/* Milliseconds of the last shyft_hip_interpolate's gather kernel (HIP events on the region's stream; the neighbour
+   table build of a new source geometry is not included). A sharded region: the slowest interpolating shard's.
+   (No reference counterpart: measurement only.) */
+double shyft_hip_last_interpolate_ms(const shyft_hip_region* h);
 /* Kernel milliseconds of the last run_cells of every shard (0 for a shard idle under the catchment filter) into
    ms[0..min(n, shards)); returns the number of shards (1 and the region's own time when unsharded). */
 size_t shyft_hip_shard_run_ms(const shyft_hip_region* h, double* ms, size_t n);

@@ -56,6 +56,7 @@ SIGNATURES = {
     "shyft_hip_run_cells_async": (C.c_int, [_h, C.c_int, C.c_int]),
     "shyft_hip_synchronize": (C.c_int, [_h]),
     "shyft_hip_last_run_ms": (C.c_double, [_h]),
+    "shyft_hip_last_interpolate_ms": (C.c_double, [_h]),
     "shyft_hip_last_run_kernel_ms": (C.c_int, [_h, C.c_void_p, C.c_int]),
     "shyft_hip_shard_run_ms": (C.c_size_t, [_h, C.c_void_p, C.c_size_t]),
     "shyft_hip_prefetch_synthetic_forcing": (C.c_int, [_h, C.c_uint64, C.c_uint64, C.c_size_t, C.c_int]),

@@ -65,6 +65,7 @@ struct shyft_hip_region {
     hipEvent_t ev_copy = nullptr;  // shyft_hip_copy_state: the copy out of this region's state has finished
     std::string err;
     double last_ms = 0.0;
+    double last_interp_ms = 0.0;  // the last interpolate's gather kernel
     int knob_instance = 0, knob_read_delay = 0;  // shyft_hip_set_test_knob (pt_gs_k launches)
 
     // host mirrors

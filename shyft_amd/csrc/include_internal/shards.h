@@ -49,6 +49,7 @@ void run_cells(shard_set* s, size_t use_ncore, int start_step, int n_steps);
 void run_cells_async(shard_set* s, int start_step, int n_steps);
 void synchronize(shard_set* s);
 double last_run_ms(const shard_set* s);
+double last_interpolate_ms(const shard_set* s);
 int last_run_kernel_ms(const shard_set* s, double* ms, int n);
 void cell_series(shard_set* s, int series, size_t cell, size_t step0, size_t n, double* buf, int write);
 void forcing_ok(shard_set* s, int* ok);

@@ -902,8 +902,13 @@ int shyft_hip_interpolate(shyft_hip_region* h, int var, size_t n_sources, const 
         g.wu = wave ? tab.wu.p : nullptr;
         g.wn = wave ? tab.wn.p : nullptr;
         g.lidx = wave ? tab.lidx.p : nullptr;
+        hip_check(hipEventRecord(h->ev0, h->stream), "hipEventRecord");
         hip_check(launch_idw_gather(g, h->stream), "idw_gather");
+        hip_check(hipEventRecord(h->ev1, h->stream), "hipEventRecord");
         hip_check(hipStreamSynchronize(h->stream), "idw");
+        float ms = 0.0f;
+        hip_check(hipEventElapsedTime(&ms, h->ev0, h->ev1), "hipEventElapsedTime");
+        h->last_interp_ms = ms;
         tab.last_path = wave ? SHYFT_HIP_IDW_WAVE : SHYFT_HIP_IDW_TILE;
     });
 }
@@ -1238,6 +1243,9 @@ int shyft_hip_synchronize(shyft_hip_region* h) {
 }
 
 double shyft_hip_last_run_ms(const shyft_hip_region* h) { return h ? (h->sh ? shards::last_run_ms(h->sh) : h->last_ms) : 0.0; }
+double shyft_hip_last_interpolate_ms(const shyft_hip_region* h) {
+    return h ? (h->sh ? shards::last_interpolate_ms(h->sh) : h->last_interp_ms) : 0.0;
+}
 
 size_t shyft_hip_shard_run_ms(const shyft_hip_region* h, double* ms, size_t n) {
     if (!h) return 0;

@@ -763,6 +763,13 @@ double last_run_ms(const shard_set* s) {
     return m;
 }
 
+double last_interpolate_ms(const shard_set* s) {
+    double m = 0.0;
+    for (size_t k = 0; k < s->S(); ++k)
+        if (!s->idle[k]) m = std::max(m, shyft_hip_last_interpolate_ms(s->r[k]));
+    return m;
+}
+
 int last_run_kernel_ms(const shard_set* s, double* ms, int n) {
     int parts = 1;
     std::vector<double> mx(4, 0.0);

@@ -225,6 +225,10 @@ class HipRegion:
     def last_run_ms(self) -> float:
         return float(self._L.shyft_hip_last_run_ms(self.h))
 
+    def last_interpolate_ms(self) -> float:
+        """The last interpolate()'s gather kernel, ms (HIP events on the region's stream)."""
+        return float(self._L.shyft_hip_last_interpolate_ms(self.h))
+
     def last_run_kernel_ms(self) -> list:
         """The last run's kernels separately (pt_gs_k: [snow kernel, flux kernel]; other stacks: [kernel])."""
         buf = (C.c_double * 4)()

@@ -97,6 +97,25 @@ def load(variant: str = "detmath"):
     return L
 
 
+def idw_run(kind, src_xyz, src_values, dst_xyz, param, dst_slope=None, variant="detmath"):
+    """inverse_distance run_interpolation of one variable (oracle kinds: 0 temperature, 1 precipitation, 2 radiation,
+    3 wind_speed, 4 rel_hum); src_values [T][S] -> [T][N] (oracle/src/idw.hpp)."""
+    L = load(variant)
+    L.oracle_idw_run.restype = C.c_int
+    L.oracle_idw_run.argtypes = [C.c_int, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                 C.c_size_t, C.c_void_p, C.c_void_p]
+    src_xyz = np.ascontiguousarray(src_xyz, dtype=np.float64)
+    src_values = np.ascontiguousarray(src_values, dtype=np.float64)
+    dst_xyz = np.ascontiguousarray(dst_xyz, dtype=np.float64)
+    S, N, T = src_xyz.shape[0], dst_xyz.shape[0], src_values.shape[0]
+    slope = None if dst_slope is None else np.ascontiguousarray(dst_slope, dtype=np.float64)
+    out = np.empty((T, N))
+    prm = np.ascontiguousarray(param, dtype=np.float64)
+    L.oracle_idw_run(int(kind), S, _p(src_xyz), _p(src_values), N, _p(dst_xyz), None if slope is None else _p(slope),
+                     T, _p(prm), _p(out))
+    return out
+
+
 def route(q, dt_us, cell_rid, cell_dist, cell_vab, rivers, query, variant="detmath"):
     """routing::model (routing.h:347-387) on the oracle. q [T][N] avg_discharge; rivers: list of
     (id, downstream_id, distance, velocity, alpha, beta). Returns local, upstream, output [T]."""

@@ -17,20 +17,7 @@ def _p(a):
 
 
 def oracle_idw(kind, src_xyz, src_values, dst_xyz, param, dst_slope=None):
-    L = oracle_lib.load()
-    L.oracle_idw_run.restype = C.c_int
-    L.oracle_idw_run.argtypes = [C.c_int, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
-                                 C.c_size_t, C.c_void_p, C.c_void_p]
-    src_xyz = np.ascontiguousarray(src_xyz, dtype=np.float64)
-    src_values = np.ascontiguousarray(src_values, dtype=np.float64)
-    dst_xyz = np.ascontiguousarray(dst_xyz, dtype=np.float64)
-    S, N, T = src_xyz.shape[0], dst_xyz.shape[0], src_values.shape[0]
-    slope = None if dst_slope is None else np.ascontiguousarray(dst_slope, dtype=np.float64)
-    out = np.empty((T, N))
-    prm = np.ascontiguousarray(param, dtype=np.float64)
-    L.oracle_idw_run(kind, S, _p(src_xyz), _p(src_values), N, _p(dst_xyz), None if slope is None else _p(slope), T,
-                     _p(prm), _p(out))
-    return out
+    return oracle_lib.idw_run(kind, src_xyz, src_values, dst_xyz, param, dst_slope)
 
 
 def mock_param(max_distance=200000.0, max_members=20, by_equation=False, default_gradient=-0.006):

@@ -60,10 +60,15 @@ def mean(v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="ptgsk_run_kernel")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     ap.add_argument("--bench-args", default="--gpus 1 --steps 20 --warmup 5")
     ap.add_argument("--base", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--idw", action="store_true",
+                    help="summarise the five IDW gathers of each chunk (idw_wave_gather_kernel) of a --idw command into "
+                         "pmc_<workload>_idw_gather.json instead of the run kernel")
     o = ap.parse_args()
+    if o.idw:
+        return idw_main(o)
     import bench
     a = bench.parse(shlex.split(o.bench_args))
     L = bench.Layout(a, 1, 0)
@@ -103,11 +108,7 @@ def main():
     timed = launches[W:]
     tr = trace_durations(os.path.join(o.base, "prof_trace", "run_kernel_trace.csv"), o.kernel)
     algo = cells * chunk * (read_b + write_b) + cells * state_b
-    sha_path = os.path.join(o.base, "lib_sha.txt")
-    if not os.path.exists(sha_path):
-        raise SystemExit(f"{sha_path} missing: the passes must record the sha256 of the library they measured "
-                         "(tools/gpu_profile.sh)")
-    lib_sha = open(sha_path).read().strip()
+    lib_sha = _sha(o.base)
     res = {
         "lib_sha256": lib_sha,
         "command": f"python3 bench.py {o.bench_args} under rocprofv3 (tools/gpu_profile.sh: one --kernel-trace "
@@ -144,6 +145,71 @@ def main():
     print(out)
     print(json.dumps({k: res[k] for k in ("traffic_bytes_per_launch", "traffic_over_algorithmic", "valu_busy",
                                           "trace_mean_ms_timed", "trace_mean_ms_all", "calibration")}))
+
+
+def _sha(base):
+    sha_path = os.path.join(base, "lib_sha.txt")
+    if not os.path.exists(sha_path):
+        raise SystemExit(f"{sha_path} missing: the passes must record the sha256 of the library they measured "
+                         "(tools/gpu_profile.sh)")
+    return open(sha_path).read().strip()
+
+
+def idw_main(o):
+    """configs[2]'s interpolation: per chunk the five gathers (one per forcing variable, in forcing order), summed."""
+    import bench
+    a = bench.parse(shlex.split(o.bench_args))
+    L = bench.Layout(a, 1, 0)
+    cells, chunk, W = L.n, a.chunk, a.warmup
+    kname = "idw_wave_gather_kernel"
+    f = counter_rows(os.path.join(o.base, "prof_fetch", "run_counter_collection.csv"), kname)
+    w = counter_rows(os.path.join(o.base, "prof_write", "run_counter_collection.csv"), kname)
+    q = counter_rows(os.path.join(o.base, "prof_sq", "run_counter_collection.csv"), kname)
+    if not f or len(f) != len(w) or len(f) != len(q) or len(f) % 5:
+        raise SystemExit(f"gather launch counts differ across passes or are not 5 per chunk: {len(f)} {len(w)} {len(q)}")
+    seg_f = counter_rows(os.path.join(o.base, "prof_fetch", "run_counter_collection.csv"), "segment_sum_kernel")
+    seg_grid = chunk * L.n_catch * 256
+    seg_ratios = [r["FETCH_SIZE"] * 1024.0 / (cells * chunk * 8.0) for _, r, m in seg_f if m["grid"] == seg_grid]
+    fetch_corr = 1.0 / mean(seg_ratios) if seg_ratios else 2.0
+    algo = [bench.idw_gather_bytes(v, cells, chunk) for v in range(5)]
+    chunks = []
+    for c in range(len(f) // 5):
+        fb = [f[5 * c + v][1]["FETCH_SIZE"] * 1024.0 for v in range(5)]
+        wb = [w[5 * c + v][1]["WRITE_SIZE"] * 1024.0 for v in range(5)]
+        dur = [q[5 * c + v][2]["duration_ns"] * 1e-9 for v in range(5)]
+        act = [q[5 * c + v][1]["SQ_ACTIVE_INST_VALU"] for v in range(5)]
+        chunks.append({"fetch_bytes": fb, "write_bytes": wb,
+                       "traffic_bytes": [x * fetch_corr + y for x, y in zip(fb, wb)],
+                       "duration_ms": [d * 1e3 for d in dur],
+                       "valu_busy": [x * 4.0 / (SIMDS * d * CLOCK) for x, d in zip(act, dur)]})
+    timed = chunks[W:]
+    tr = trace_durations(os.path.join(o.base, "prof_trace", "run_kernel_trace.csv"), kname)
+    tr_chunks = [sum(tr[5 * c:5 * c + 5]) for c in range(len(tr) // 5)]
+    res = {
+        "lib_sha256": _sha(o.base),
+        "command": f"python3 bench.py {o.bench_args} under rocprofv3 (tools/gpu_profile.sh passes)",
+        "workload": bench.workload_tag(a, cells), "kernel": kname, "cells": cells, "chunk": chunk, "warmup": W,
+        "calibration": {"fetch_correction": fetch_corr, "write_correction": 1.0,
+                        "note": "FETCH correction from the same run's catchment segment sums (8 B/cell-step read); "
+                                "WRITE_SIZE as counted (the guide: exact on gfx950)"},
+        "algorithmic_bytes_by_variable": algo,
+        "traffic_bytes_by_variable": [mean([c["traffic_bytes"][v] for c in timed]) for v in range(5)],
+        "traffic_bytes_per_launch_sum": mean([sum(c["traffic_bytes"]) for c in timed]),
+        "valu_busy_by_variable": [mean([c["valu_busy"][v] for c in timed]) for v in range(5)],
+        "valu_busy": mean([sum(b * d for b, d in zip(c["valu_busy"], c["duration_ms"])) / sum(c["duration_ms"])
+                           for c in timed]),
+        "trace_mean_ms_by_variable": [mean(tr[5 * W + v::5]) for v in range(5)],
+        "trace_mean_ms_chunk_timed": mean(tr_chunks[W:]),
+        "chunks": chunks,
+    }
+    res["traffic_over_algorithmic"] = res["traffic_bytes_per_launch_sum"] / sum(algo)
+    out_dir = os.path.join(ROOT, "profiles", o.round)
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"pmc_{res['workload']}_idw_gather.json")
+    json.dump(res, open(out, "w"), indent=1)
+    print(out)
+    print(json.dumps({k: res[k] for k in ("traffic_over_algorithmic", "valu_busy", "valu_busy_by_variable",
+                                          "trace_mean_ms_by_variable", "trace_mean_ms_chunk_timed")}))
 
 
 if __name__ == "__main__":
