@@ -59,6 +59,12 @@ constexpr int BLOCK = 256;
 // The solving wavefronts run at issue priority 3 (measured: 135.3 -> 134.5 ms per chunk).
 constexpr int JOB_PRIO = 3;
 
+// Priestley-Taylor / Kirchner with the inline exp / log (kmath<true>, as pt_gs_k) instead of the out-of-line calls
+#ifndef SHYFT_PTSSK_INLINE_MATH
+#define SHYFT_PTSSK_INLINE_MATH 1  // r06: 80.5 -> 79.4 ms per 730-step chunk, year mean (profiles/r06/ptssk_variants_g.txt)
+#endif
+constexpr bool PTSSK_INLINE_MATH = SHYFT_PTSSK_INLINE_MATH != 0;
+
 // r06: a step with few jobs gives each job a group of L lanes of the solving wavefronts (ss_sca_rel_red<L>,
 // device/ptssk_dev.h: lgammas, opening evaluations and final cdfs side by side, the bisection 2-3 levels per
 // round), as long as the step's jobs fit GROUP_LANES lanes; the same bits as one lane per job
@@ -274,11 +280,11 @@ void ptssk_run_kernel(const ptssk_kargs a) {
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
         double ae_exp;  // actual_evapotranspiration's exp, evaluated beside Priestley-Taylor's (pt_pot_evap_exp)
-        const double pot_evap = pt_pot_evap_exp(pt_albedo, pt_alpha, temp, rad, rel_hum, -q * 3.0 / ae_scale, ae_exp) * 3600.0;
+        const double pot_evap = pt_pot_evap_exp<PTSSK_INLINE_MATH>(pt_albedo, pt_alpha, temp, rad, rel_hum, -q * 3.0 / ae_scale, ae_exp) * 3600.0;
         const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(s.sca, glacier_fraction));
         const double gm_mmh = gm_melt_m3s / (mmh_to_m3s_scale_factor * cell_area_m2);
         double q_avg;
-        if (!kirchner_step(q, q_avg, snow_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
+        if (!kirchner_step<PTSSK_INLINE_MATH>(q, q_avg, snow_outflow * snow_storage_fraction + prec * kirchner_routed_prec + gm_routed * gm_mmh,
                            ae, a.t1_hours, kc1, kc2, kc3))
             err = ERR_KIRCHNER_MAX_ITER;
         const double total_discharge = smax(0.0, prec - ae) * direct_response_fraction + gm_direct * gm_mmh +
