@@ -11,8 +11,8 @@
 // Algorithms (restated from the standard literature):
 //   exp  : Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-13 Taylor in
 //          Horner form, scaling by 2^k through the exponent bits.
-//   log  : x = 2^e m, m in [sqrt(1/2), sqrt(2)), s = (m-1)/(m+1),
-//          log m = 2 atanh(s) evaluated in double-double for the leading terms.
+//   log  : x = 2^k (1+f), 1+f in [sqrt(1/2), sqrt(2)), s = f/(2+f), fdlibm's e_log.c polynomial (one division);
+//          pow and lgamma use log_dd: log m = 2 atanh(s) in double-double for the leading terms.
 //   pow  : exp(y * log x) with log x carried as a double-double.
 //   lgamma (x > 0): Stirling series with 8 Bernoulli terms for x >= 10; upward
 //          recurrence lgamma(x) = lgamma(x+n) - log(x (x+1) ... (x+n-1)) below.
@@ -142,7 +142,7 @@ DM_FN double exp(double x) {
 }
 
 // ---------------------------------------------------------------- log (double-double core)
-// log(x) = hi + lo for finite x > 0 (normal or subnormal)
+// log(x) = hi + lo for finite x > 0 (normal or subnormal): pow's and lgamma's double-double log
 DM_FN void log_dd(double x, double& hi, double& lo) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -165,7 +165,11 @@ DM_FN void log_dd(double x, double& hi, double& lo) {
     const double d = 2.0 + f;
     const double d_lo = (2.0 - d) + f;  // fast two-sum (|2| >= |f|)
     const double s = f / d;
+#ifdef DM_ABLATE_LOG_SLO  // timing ablation only (wrong results)
+    const double s_lo = 0.0 * d_lo;
+#else
     const double s_lo = (DM_FMA(-s, d, f) - s * d_lo) / d;
+#endif
     const double z = s * s;
     // 2 atanh(s) = 2s + s^3 * (2/3 + 2/5 z + 2/7 z^2 + ...); |s| <= 0.1716, z <= 0.02944
     double t = 2.0 / 25;
@@ -197,23 +201,54 @@ DM_FN void log_dd(double x, double& hi, double& lo) {
     lo = small - (hi - sum);
 }
 
+// log(x) = k ln2 + log(1 + f) for positive normal finite x: the method of fdlibm's e_log.c (one division) -- 1 + f
+// in [sqrt(2)/2, sqrt(2)), s = f / (2 + f), log(1 + f) = f - hfsq + s (hfsq + R(s^2)) with fdlibm's 7-term minimax R,
+// here evaluated with fused multiply-adds; k_adj: an exponent the caller removed (subnormal scaling). Within 1 ulp of
+// glibc (tests/test_detmath.py). r06: replaces log_dd's hi part (a double-double atanh series with two divisions:
+// one division fewer on every log of every stack; log_dd stays for pow and lgamma, which use its low part).
+constexpr double LOG_LG1 = 6.666666666666735130e-01, LOG_LG2 = 3.999999999940941908e-01,
+                 LOG_LG3 = 2.857142874366239149e-01, LOG_LG4 = 2.222219843214978396e-01,
+                 LOG_LG5 = 1.818357216161805012e-01, LOG_LG6 = 1.531383769920937332e-01,
+                 LOG_LG7 = 1.479819860511658591e-01;
+DM_FN double log_core(double x, int k_adj) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    const double LN2_HI = 6.93147180369123816490e-01;  // upper 32 bits of ln2: dk * LN2_HI is exact
+    const double LN2_LO = 1.90821492927058770002e-10;
+    uint64_t u = as_u64(x);
+    int k = (int)((u >> 52) & 0x7ff) - 1023 + k_adj;
+    const uint32_t hx = (uint32_t)(u >> 32) & 0x000fffffu;
+    const uint32_t i = (hx + 0x95f64u) & 0x100000u;  // 1 + f >= sqrt(2): halve it
+    u = (u & 0x000fffffffffffffull) | ((uint64_t)(i ^ 0x3ff00000u) << 32);
+    k += (int)(i >> 20);
+    const double f = as_f64(u) - 1.0;
+    const double s = f / (2.0 + f);
+    const double dk = (double)k;
+    const double z = s * s;
+    const double w = z * z;
+    const double t1 = w * DM_FMA(w, DM_FMA(w, LOG_LG6, LOG_LG4), LOG_LG2);
+    const double t2 = z * DM_FMA(w, DM_FMA(w, DM_FMA(w, LOG_LG7, LOG_LG5), LOG_LG3), LOG_LG1);
+    const double R = t2 + t1;
+    if (((int32_t)(hx - 0x6147au) | (int32_t)(0x6b851u - hx)) > 0) {
+        const double hfsq = 0.5 * f * f;
+        return dk * LN2_HI - ((hfsq - DM_FMA(s, hfsq + R, dk * LN2_LO)) - f);
+    }
+    return dk * LN2_HI - (DM_FMA(s, f - R, -(dk * LN2_LO)) - f);
+}
+
 // every x (NaN, negative, zero, infinity, subnormal)
 DM_COLD DM_FN double log_general(double x) {
     if (is_nan(x)) return x;
     if (x < 0.0) return qnan();
     if (x == 0.0) return -inf();
     if (x == inf()) return x;
-    double hi, lo;
-    log_dd(x, hi, lo);
-    return hi;
+    if (x < 2.2250738585072014e-308) return log_core(x * 18014398509481984.0, -54);  // subnormal: scale by 2^54
+    return log_core(x, 0);
 }
 
 DM_FN double log(double x) {
-    if (x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308) {  // positive, normal, finite
-        double hi, lo;
-        log_dd(x, hi, lo);  // (its subnormal branch is not taken)
-        return hi;
-    }
+    if (x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308) return log_core(x, 0);  // positive normal
     return log_general(x);
 }
 

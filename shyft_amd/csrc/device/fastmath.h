@@ -7,16 +7,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../../detmath/detmath.h"
+
 namespace shyft_dev {
 
-// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: 2/25 .. 2/3, LN2_HI LN2_LO
+// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: LN2_HI LN2_LO and detmath::log_core's Lg1 .. Lg7
 static __constant__ double gsb_const[32] = {
     1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
     1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
     2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04, 1.3888888888888889e-03,
     8.3333333333333333e-03, 4.1666666666666664e-02, 1.6666666666666666e-01,
-    2.0 / 25, 2.0 / 23, 2.0 / 21, 2.0 / 19, 2.0 / 17, 2.0 / 15, 2.0 / 13, 2.0 / 11, 2.0 / 9, 2.0 / 7, 2.0 / 5,
-    2.0 / 3, 0.0, 0.0, 0.0, 0.0, 0.0};
+    detmath::LOG_LG1, detmath::LOG_LG2, detmath::LOG_LG3, detmath::LOG_LG4, detmath::LOG_LG5, detmath::LOG_LG6,
+    detmath::LOG_LG7, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 
 typedef __attribute__((address_space(4))) const double gsb_cdouble;
 
@@ -28,7 +30,7 @@ __device__ __forceinline__ double gs_fma_s(double a, double b, double c) {
 }
 
 struct gsb_k {
-    double c[27];
+    double c[22];
 };
 
 __device__ __forceinline__ gsb_k gsb_load() {
@@ -36,7 +38,7 @@ __device__ __forceinline__ gsb_k gsb_load() {
     const gsb_cdouble* __restrict__ p = (const gsb_cdouble*)gsb_const;
     asm volatile("" : "+s"(p));  // keep the table opaque: scalar loads into SGPRs, not folded literals
 #pragma unroll
-    for (int i = 0; i < 27; ++i) k.c[i] = p[i];
+    for (int i = 0; i < 22; ++i) k.c[i] = p[i];
     return k;
 }
 
@@ -55,34 +57,27 @@ __device__ __forceinline__ double gsb_exp(double x, const gsb_k& k) {
     return __builtin_ldexp(p, (int)kf);
 }
 
-// detmath::log for positive normal finite x (log_dd without its subnormal branch, hi part)
+// detmath::log for positive normal finite x (detmath::log_core with k_adj = 0, step by step)
 __device__ __forceinline__ double gsb_log(double x, const gsb_k& k) {
-    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    uint64_t u = (uint64_t)__double_as_longlong(x);
     int e = (int)((u >> 52) & 0x7ff) - 1023;
-    double m = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
-    if (m > 1.4142135623730951) {
-        m = m * 0.5;
-        e += 1;
-    }
-    const double f = m - 1.0;
-    const double d = 2.0 + f;
-    const double d_lo = (2.0 - d) + f;
-    const double s = f / d;
-    const double s_lo = (__builtin_fma(-s, d, f) - s * d_lo) / d;
+    const uint32_t hx = (uint32_t)(u >> 32) & 0x000fffffu;
+    const uint32_t i = (hx + 0x95f64u) & 0x100000u;
+    u = (u & 0x000fffffffffffffull) | ((uint64_t)(i ^ 0x3ff00000u) << 32);
+    e += (int)(i >> 20);
+    const double f = __longlong_as_double((long long)u) - 1.0;
+    const double s = f / (2.0 + f);
+    const double dk = (double)e;
     const double z = s * s;
-    double t = gs_fma_s(k.c[15], z, k.c[16]);
-#pragma unroll
-    for (int i = 17; i <= 26; ++i) t = gs_fma_s(t, z, k.c[i]);
-    const double tail = (s * z) * t;
-    const double ed = (double)e;
-    const double a_hi = ed * k.c[2];
-    const double a_lo = ed * k.c[3];
-    const double b = 2.0 * s;
-    const double sum = a_hi + b;
-    const double bb = sum - a_hi;
-    const double err = (a_hi - (sum - bb)) + (b - bb);
-    const double small = ((err + 2.0 * s_lo) + tail) + a_lo;
-    return sum + small;
+    const double w = z * z;
+    const double t1 = w * gs_fma_s(w, gs_fma_s(w, k.c[20], k.c[18]), k.c[16]);
+    const double t2 = z * gs_fma_s(w, gs_fma_s(w, gs_fma_s(w, k.c[21], k.c[19]), k.c[17]), k.c[15]);
+    const double R = t2 + t1;
+    if (((int32_t)(hx - 0x6147au) | (int32_t)(0x6b851u - hx)) > 0) {
+        const double hfsq = 0.5 * f * f;
+        return dk * k.c[2] - ((hfsq - __builtin_fma(s, hfsq + R, dk * k.c[3])) - f);
+    }
+    return dk * k.c[2] - (__builtin_fma(s, f - R, -(dk * k.c[3])) - f);
 }
 
 }  // namespace shyft_dev
