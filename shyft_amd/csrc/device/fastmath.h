@@ -11,12 +11,12 @@
 
 namespace shyft_dev {
 
-// exp: INV_LN2 SHIFT LN2_HI LN2_LO, Taylor 1/13! .. 1/3!; log: LN2_HI LN2_LO and detmath::log_core's Lg1 .. Lg7
+// exp: INV_LN2 SHIFT LN2_HI LN2_LO and detmath::exp_poly's q coefficients; log: LN2_HI LN2_LO and
+// detmath::log_core's Lg1 .. Lg7
 static __constant__ double gsb_const[32] = {
     1.4426950408889634, 6755399441055744.0, 6.93147180369123816490e-01, 1.90821492927058770002e-10,
-    1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
-    2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04, 1.3888888888888889e-03,
-    8.3333333333333333e-03, 4.1666666666666664e-02, 1.6666666666666666e-01,
+    detmath::EXP_Q[0], detmath::EXP_Q[1], detmath::EXP_Q[2], detmath::EXP_Q[3], detmath::EXP_Q[4], detmath::EXP_Q[5],
+    detmath::EXP_Q[6], detmath::EXP_Q[7], detmath::EXP_Q[8], detmath::EXP_Q[9], detmath::EXP_Q[10],
     detmath::LOG_LG1, detmath::LOG_LG2, detmath::LOG_LG3, detmath::LOG_LG4, detmath::LOG_LG5, detmath::LOG_LG6,
     detmath::LOG_LG7, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 
@@ -44,17 +44,14 @@ __device__ __forceinline__ gsb_k gsb_load() {
 
 // detmath::exp for |x| <= 708 (exp_poly + one ldexp)
 __device__ __forceinline__ double gsb_exp(double x, const gsb_k& k) {
-    const double t = x * k.c[0] + k.c[1];
+    const double t = gs_fma_s(x, k.c[0], k.c[1]);
     const double kf = t - k.c[1];
     double r = __builtin_fma(-kf, k.c[2], x);
     r = __builtin_fma(-kf, k.c[3], r);
-    double p = gs_fma_s(r, k.c[4], k.c[5]);
+    double q = gs_fma_s(r, k.c[4], k.c[5]);
 #pragma unroll
-    for (int i = 6; i <= 14; ++i) p = gs_fma_s(p, r, k.c[i]);
-    p = __builtin_fma(p, r, 0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
-    return __builtin_ldexp(p, (int)kf);
+    for (int i = 6; i <= 14; ++i) q = gs_fma_s(q, r, k.c[i]);
+    return __builtin_ldexp(__builtin_fma(r, q, 1.0), (int)kf);
 }
 
 // detmath::log for positive normal finite x (detmath::log_core with k_adj = 0, step by step)

@@ -60,23 +60,20 @@ __device__ __noinline__ dexp_pair dexp2(double x, double y) {
     if (__builtin_fabs(x) <= 708.0 && __builtin_fabs(y) <= 708.0) {
 #pragma clang fp contract(off)
         // detmath::exp_poly on both arguments, step by step side by side
-        const double tx = x * 1.4426950408889634 + 6755399441055744.0, ty = y * 1.4426950408889634 + 6755399441055744.0;
+        const double tx = __builtin_fma(x, 1.4426950408889634, 6755399441055744.0),
+                     ty = __builtin_fma(y, 1.4426950408889634, 6755399441055744.0);
         const double kx = tx - 6755399441055744.0, ky = ty - 6755399441055744.0;
         double rx = __builtin_fma(-kx, 6.93147180369123816490e-01, x), ry = __builtin_fma(-ky, 6.93147180369123816490e-01, y);
         rx = __builtin_fma(-kx, 1.90821492927058770002e-10, rx);
         ry = __builtin_fma(-ky, 1.90821492927058770002e-10, ry);
-        const double C[13] = {1.6059043836821614e-10, 2.0876756987868099e-09, 2.5052108385441720e-08,
-                              2.7557319223985893e-07, 2.7557319223985888e-06, 2.4801587301587302e-05,
-                              1.9841269841269841e-04, 1.3888888888888889e-03, 8.3333333333333333e-03,
-                              4.1666666666666664e-02, 1.6666666666666666e-01, 0.5, 1.0};
-        double px = C[0], py = C[0];
+        double px = detmath::EXP_Q[0], py = detmath::EXP_Q[0];
 #pragma unroll
-        for (int i = 1; i < 13; ++i) {
-            px = __builtin_fma(px, rx, C[i]);
-            py = __builtin_fma(py, ry, C[i]);
+        for (int i = 1; i < 11; ++i) {
+            px = __builtin_fma(px, rx, detmath::EXP_Q[i]);
+            py = __builtin_fma(py, ry, detmath::EXP_Q[i]);
         }
-        px = __builtin_fma(px, rx, 1.0);
-        py = __builtin_fma(py, ry, 1.0);
+        px = __builtin_fma(rx, px, 1.0);
+        py = __builtin_fma(ry, py, 1.0);
         r.a = __builtin_ldexp(px, (int)kx);
         r.b = __builtin_ldexp(py, (int)ky);
     } else {
