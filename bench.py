@@ -630,6 +630,54 @@ def pmc_summary(a, cells, suffix=""):
     return d, None
 
 
+SEASONS = (("winter (Dec-Feb)", (12, 1, 2)), ("spring (Mar-May)", (3, 4, 5)), ("summer (Jun-Aug)", (6, 7, 8)),
+           ("autumn (Sep-Nov)", (9, 10, 11)))
+
+
+def _chunk_month(step0, n):
+    """calendar month (1-12) of the middle of steps [step0, step0 + n) of the synthetic year (2015, hourly)"""
+    import datetime
+    mid = datetime.datetime(2015, 1, 1) + datetime.timedelta(hours=(step0 + n / 2.0) % YEAR)
+    return mid.month
+
+
+def instruction_budget(a, pmc, timed, cells, chunk):
+    """the run kernel's VALU lane-instructions per cell-step by season (SQ_INSTS_VALU of each
+    timed launch of the PMC pass), by instruction class (the SQ_INSTS_VALU_* pass), and -- pt_gs_k -- next to the CPU
+    oracle's fp64 operation count for the same steps (tools/mb/ptgsk_opcount.cpp: every add / mul / div / fma of the
+    restatement counted as it runs, on 1024 cells of the same region)."""
+    per = 64.0 / (cells * chunk)
+    months = [_chunk_month(k * chunk, chunk) for k in range(len(timed))]
+    by_season = {}
+    for name, ms in SEASONS:
+        v = [l["SQ_INSTS_VALU"] * per for l, m in zip(timed, months) if m in ms]
+        if v:
+            by_season[name] = round(float(np.mean(v)), 1)
+    out = {"lane_instr_per_cell_step_by_season": by_season}
+    if "valu_lane_instr_per_cell_step_by_class" in pmc:
+        out["lane_instr_per_cell_step_by_class"] = {k: round(v, 1) for k, v in
+                                                   pmc["valu_lane_instr_per_cell_step_by_class"].items()}
+    if a.stack == "pt_gs_k" and not a.idw and chunk == CHUNK:
+        try:
+            oc = json.load(open(os.path.join(PROFILE_DIR, "ptgsk_oracle_opcount_1024cells.json")))
+        except (OSError, ValueError):
+            return out
+        rows = oc["per_cell_step_by_chunk"]
+        ops = {}
+        for name, ms in SEASONS:
+            v = [r["add"] + r["mul"] + r["div"] + r["fma"] + r["sqrt"] for k, r in enumerate(rows)
+                 if _chunk_month(k * chunk, chunk) in ms]
+            d = [r["div"] for k, r in enumerate(rows) if _chunk_month(k * chunk, chunk) in ms]
+            if v:
+                ops[name] = {"fp64_ops": round(float(np.mean(v)), 1), "of_which_divisions": round(float(np.mean(d)), 1)}
+        out["oracle_fp64_ops_per_cell_step_by_season"] = ops
+        out["oracle_fp64_ops_source"] = (f"profiles/{os.path.basename(PROFILE_DIR)}/ptgsk_oracle_opcount_1024cells.json "
+                                         "(tools/mb/ptgsk_opcount.cpp: the oracle with a counting double type, 1024 "
+                                         "cells of the bench region, the same 438-step chunks); a division is one "
+                                         "operation there and about ten VALU instructions on gfx950")
+    return out
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -899,6 +947,7 @@ def main():
             "busy": act * 4.0 / (1024 * 2.4e9 * avg_kernel_ms * 1e-3),
             "wave_instr_per_launch": ins,
             "lane_instr_per_cell_step": ins * 64.0 / (cells * chunk),
+            **instruction_budget(a, pmc, timed, cells, chunk),
             "by_chunk_busy": [round(l["valu_busy"], 3) for l in timed],
             "profile_kernel_ms": pmc["trace_mean_ms_timed"],
             "source": f"profiles/{os.path.basename(PROFILE_DIR)}/pmc_{workload_tag(a, cells)}.json (rocprofv3 SQ "

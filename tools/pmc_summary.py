@@ -96,15 +96,21 @@ def main():
     fetch_corr = 1.0 / fetch_ratio if fetch_ratio else 2.0
     write_corr = 1.0 / write_ratio if write_ratio else 1.0
 
+    # optional pass 5: VALU instructions by class (tools/gpu_profile.sh "sqf")
+    qf_path = os.path.join(o.base, "prof_sqf", "run_counter_collection.csv")
+    qf = counter_rows(qf_path, o.kernel) if os.path.exists(qf_path) else []
+    if qf and len(qf) != len(f):
+        raise SystemExit(f"VALU-class pass launch count {len(qf)} != {len(f)}")
     launches = []
-    for (df, cf, mf), (dw, cw, mw), (dq, cq, mq) in zip(f, w, q):
+    for n_l, ((df, cf, mf), (dw, cw, mw), (dq, cq, mq)) in enumerate(zip(f, w, q)):
         fb = cf["FETCH_SIZE"] * 1024.0
         wb = cw["WRITE_SIZE"] * 1024.0
         dur = mq["duration_ns"] * 1e-9
         launches.append({"dispatch": [df, dw, dq], "fetch_bytes": fb, "write_bytes": wb,
                          "traffic_bytes": fb * fetch_corr + wb * write_corr,
                          "sq_duration_ns": mq["duration_ns"],
-                         "valu_busy": cq["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * dur * CLOCK), **cq, **mq})
+                         "valu_busy": cq["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * dur * CLOCK), **cq, **mq,
+                         **({("class_" + k): v for k, v in qf[n_l][1].items()} if qf else {})})
     timed = launches[W:]
     tr = trace_durations(os.path.join(o.base, "prof_trace", "run_kernel_trace.csv"), o.kernel)
     algo = cells * chunk * (read_b + write_b) + cells * state_b
@@ -134,6 +140,15 @@ def main():
         "launches": launches,
     }
     res["traffic_over_algorithmic"] = res["traffic_bytes_per_launch"] / algo
+    if qf:
+        # lane-instructions per cell-step by class, mean over the timed launches (wave instructions x 64 lanes)
+        per = 64.0 / (cells * chunk)
+        cls = {"fp64_add": "SQ_INSTS_VALU_ADD_F64", "fp64_mul": "SQ_INSTS_VALU_MUL_F64",
+               "fp64_fma": "SQ_INSTS_VALU_FMA_F64", "fp64_trans": "SQ_INSTS_VALU_TRANS_F64",
+               "int32": "SQ_INSTS_VALU_INT32", "int64": "SQ_INSTS_VALU_INT64", "cvt": "SQ_INSTS_VALU_CVT"}
+        res["valu_lane_instr_per_cell_step_by_class"] = {
+            k: mean([l["class_" + c] for l in timed]) * per for k, c in cls.items()}
+        res["valu_lane_instr_per_cell_step_by_class"]["all"] = mean([l["class_SQ_INSTS_VALU"] for l in timed]) * per
     out_dir = os.path.join(ROOT, "profiles", o.round)
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, f"pmc_{res['workload']}.json")
