@@ -363,8 +363,14 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
 // This never-launched 8-wave caller makes that range tight: the callees are register-allocated for 64 VGPRs, so
 // they clobber fewer registers and the 4-wave step loop keeps more values live across its calls (VGPR spills of
 // the bench instance 164 -> 127). Measured on the 1M-cell bench year, 730-step chunks: 105.3 -> 100.0 ms per chunk,
-// bit-exact (tools/ptgsk_variants.py).
-__global__ __launch_bounds__(256, 8) void ptgsk_callee_budget_kernel(const ptgsk_kargs a) {
+// bit-exact (tools/ptgsk_variants.py). Round 6 re-measured the budget against the current step
+// (detmath's one-division log and degree-11 exp): 7 waves (72 VGPRs for the callees) 75.5 -> 74.2 ms per chunk,
+// 6 waves 74.8, bit-exact (profiles/r06/ptgsk_budget_variants.txt); the caller spills a few more VGPRs (32 -> 39)
+// but saves more in the calls.
+#ifndef SHYFT_PTGSK_BUDGET_WAVES
+#define SHYFT_PTGSK_BUDGET_WAVES 7
+#endif
+__global__ __launch_bounds__(256, SHYFT_PTGSK_BUDGET_WAVES) void ptgsk_callee_budget_kernel(const ptgsk_kargs a) {
     if (a.n_cells >= 0) return;  // never runs: launch_ptgsk_run only references it
     const int c = threadIdx.x;
     gs_state s{};
