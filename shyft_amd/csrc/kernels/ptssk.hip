@@ -15,6 +15,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifdef SHYFT_PROF
+// phase timing (profiling builds only, tools/ptssk_phases.py): per-wavefront s_memtime deltas summed over the launch;
+// [0..5] front / queue + first barrier / job compute / second barrier / ss_back + glacier / PT + AE + kirchner +
+// stores, [8] solver-wavefront job cycles, [9] solver wavefront-steps, [10] job lanes of those wavefront-steps,
+// [11..15] inside a job (device/ptssk_dev.h SS_JOB_MARK): lgammas / opening evaluations / Brent + walk / bisection /
+// final cdfs
+__device__ unsigned long long g_ptssk_prof[16];
+extern "C" int shyft_ptssk_prof_read(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptssk_prof), sizeof(g_ptssk_prof)) != hipSuccess) return 1;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ptssk_prof), z, sizeof z) != hipSuccess;
+}
+#define SS_JOB_T0() unsigned long long ss_jt_ = __builtin_amdgcn_s_memtime()
+#define SS_JOB_MARK(k)                                                                                      \
+    do {                                                                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                         \
+        if (__lane_id() == (unsigned)(__ffsll((unsigned long long)__ballot(1)) - 1))                        \
+            atomicAdd(&g_ptssk_prof[11 + (k)], t_ - ss_jt_);                                                \
+        ss_jt_ = t_;                                                                                        \
+    } while (0)
+#endif
+
 #include "../device/pt_dev.h"
 #include "../device/ptgsk_dev.h"
 #include "../device/ptssk_dev.h"
@@ -24,15 +46,6 @@
 using namespace shyft_dev;
 
 #ifdef SHYFT_PROF
-// phase timing (profiling builds only, tools/ptssk_phases.py): per-wavefront s_memtime deltas summed over the launch;
-// [0..4] front / queue + first barrier / job compute / second barrier / back + PT + AE + kirchner + stores,
-// [8] solver-wavefront job cycles, [9] solver wavefront-steps, [10] job lanes of those wavefront-steps
-__device__ unsigned long long g_ptssk_prof[12];
-extern "C" int shyft_ptssk_prof_read(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptssk_prof), sizeof(g_ptssk_prof)) != hipSuccess) return 1;
-    unsigned long long z[12] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_ptssk_prof), z, sizeof z) != hipSuccess;
-}
 #define PROF_DECL unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long prof_t = __builtin_amdgcn_s_memtime();
 #define PROF_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[k] += t_ - prof_t; prof_t = t_; } while (0)
 #define PROF_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 6; ++k_) atomicAdd(&g_ptssk_prof[k_], prof_acc[k_]); } while (0)
@@ -279,6 +292,7 @@ void ptssk_run_kernel(const ptssk_kargs a) {
         double gm_melt_m3s = 0.0;
         if (!(glacier_area_m2 <= sca_area || temp <= 0.0))
             gm_melt_m3s = dtf * temp * (glacier_area_m2 - sca_area) * (0.001 / 86400.0);
+        PROF_MARK(4);  // ss_back + glacier
         double ae_exp;  // actual_evapotranspiration's exp, evaluated beside Priestley-Taylor's (pt_pot_evap_exp)
         const double pot_evap = pt_pot_evap_exp<PTSSK_INLINE_MATH>(pt_albedo, pt_alpha, temp, rad, rel_hum, -q * 3.0 / ae_scale, ae_exp) * 3600.0;
         const double ae = pot_evap * (1.0 - ae_exp) * (1.0 - smax(s.sca, glacier_fraction));
@@ -306,7 +320,7 @@ void ptssk_run_kernel(const ptssk_kargs a) {
             R[PR_PE_OUTPUT * RS + fo] = pot_evap;
         }
         if (SS && i + 1 == i_end) collect_state(wi + 1);
-        PROF_MARK(4);
+        PROF_MARK(5);
     }
     PROF_FLUSH();
     if (!valid) return;

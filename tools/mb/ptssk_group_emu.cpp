@@ -2,7 +2,8 @@
 // replayed against the oracle's boost::math::tools::bisect restatement (oracle/src/ptssk.hpp) on recorded jobs:
 //  1. the grouped rounds: the midpoints of the next D levels evaluated at once (D = 2: groups of 4 lanes; D = 3: 8),
 //     then the sequential loop replayed over them;
-//  2. ss_zero_sign: the midpoint's sign without the pdfs' divisions where it is certain.
+//  2. ss_zero_sign: the midpoint's sign without the pdfs' divisions where it is certain, and (r06) without the exps
+//     where their arguments decide it -- each such decision also checked against the full evaluation.
 // Both must end on the oracle's bracket, bit for bit, for every job.
 // jobs: tools/mb/ptssk_jobs -o jobs.bin (u, n, nu_a, alpha, ... per row of 9 doubles)
 // build: g++ -O2 -std=c++17 -mfma -ffp-contract=off -o tools/mb/ptssk_group_emu tools/mb/ptssk_group_emu.cpp
@@ -22,7 +23,7 @@ int main(int argc, char** argv) {
     while (fread(row, sizeof(double), 9, f) == 9) J.insert(J.end(), row, row + 9);
     fclose(f);
     const size_t nr = J.size() / 9;
-    long bad_group[4] = {0}, bad_sign = 0, fast = 0, slow = 0, checked = 0;
+    long bad_group[4] = {0}, bad_sign = 0, fast = 0, slow = 0, checked = 0, exp_skipped = 0, bad_skip = 0;
     for (size_t r = 0; r < nr; ++r) {
         const double* q = &J[9 * r];
         const unsigned long u = (unsigned long)q[0], n = (unsigned long)q[1];
@@ -33,15 +34,32 @@ int main(int argc, char** argv) {
         auto zf = [&](double x) { return g_m.pdf(x) - g_a.pdf(x); };
         auto zs = [&](double x) {  // ss_zero_sign (x > 0 here)
             const double z = x / theta, lz = OLOG(z);
-            const double ea = OEXP(nu_m * lz - z - lg_m), eb = OEXP(nu_a * lz - z - lg_a);
-            if (ea == 0 && eb == 0) { ++fast; return 0.0; }
-            const double LO = 0x1p-960, HI = 0x1p960;
-            if (z >= 0x1p-30 && z <= 0x1p30 && theta >= 0x1p-30 && theta <= 0x1p30) {
-                if (eb >= LO && eb <= HI && eb > ea * (1.0 + 0x1p-48)) { ++fast; return -1.0; }
-                if (ea >= LO && ea <= HI && ea > eb * (1.0 + 0x1p-48)) { ++fast; return 1.0; }
+            const double A = nu_m * lz - z - lg_m, B = nu_a * lz - z - lg_a;
+            const bool in_range = z >= 0x1p-30 && z <= 0x1p30 && theta >= 0x1p-30 && theta <= 0x1p30;
+            double skip = 2.0;  // the exp-argument decision (r06), checked against the full evaluation below
+            if (A < -745.1332191019412 && B < -745.1332191019412) {
+                skip = 0.0;
+            } else if (in_range) {
+                const double hi = A > B ? A : B;
+                if (hi >= -660.0 && hi <= 660.0) {
+                    if (B - A > 0x1p-40) skip = -1.0;
+                    else if (A - B > 0x1p-40) skip = 1.0;
+                }
             }
-            ++slow;
-            return ea / z / theta - eb / z / theta;
+            const double ea = OEXP(A), eb = OEXP(B);
+            double full;
+            const double LO = 0x1p-960, HI = 0x1p960;
+            if (ea == 0 && eb == 0) full = 0.0;
+            else if (in_range && eb >= LO && eb <= HI && eb > ea * (1.0 + 0x1p-48)) full = -1.0;
+            else if (in_range && ea >= LO && ea <= HI && ea > eb * (1.0 + 0x1p-48)) full = 1.0;
+            else full = ea / z / theta - eb / z / theta;
+            if (skip != 2.0) {
+                ++exp_skipped;
+                if (skip != full) ++bad_skip;
+                return skip;
+            }
+            if (full == 1.0 || full == -1.0 || full == 0.0) ++fast; else ++slow;
+            return full;
         };
         double lower = g_m.mean();
         uintmax_t bi = ~0ull;
@@ -98,7 +116,8 @@ int main(int argc, char** argv) {
         }
     }
     printf("jobs %zu, bisections checked %ld: differing brackets: sign surrogate %ld, D=2 %ld, D=3 %ld; "
-           "surrogate evaluations without the divisions %ld, with %ld\n",
-           nr, checked, bad_sign, bad_group[2], bad_group[3], fast, slow);
-    return (bad_sign || bad_group[2] || bad_group[3]) ? 1 : 0;
+           "surrogate evaluations decided by the exp arguments %ld (differing from the exps' decision: %ld), by the exps "
+           "without the divisions %ld, with the divisions %ld\n",
+           nr, checked, bad_sign, bad_group[2], bad_group[3], exp_skipped, bad_skip, fast, slow);
+    return (bad_sign || bad_group[2] || bad_group[3] || bad_skip) ? 1 : 0;
 }
