@@ -7,6 +7,7 @@
 // Both must end on the oracle's bracket, bit for bit, for every job.
 // jobs: tools/mb/ptssk_jobs -o jobs.bin (u, n, nu_a, alpha, ... per row of 9 doubles)
 // build: g++ -O2 -std=c++17 -mfma -ffp-contract=off -o tools/mb/ptssk_group_emu tools/mb/ptssk_group_emu.cpp
+#include <cmath>
 #include <cstdio>
 #include <vector>
 
@@ -23,7 +24,7 @@ int main(int argc, char** argv) {
     while (fread(row, sizeof(double), 9, f) == 9) J.insert(J.end(), row, row + 9);
     fclose(f);
     const size_t nr = J.size() / 9;
-    long bad_group[4] = {0}, bad_sign = 0, fast = 0, slow = 0, checked = 0, exp_skipped = 0, bad_skip = 0;
+    long bad_group[4] = {0}, bad_sign = 0, fast = 0, slow = 0, checked = 0, exp_skipped = 0, bad_skip = 0, flog_decided = 0, flog_fallback = 0, bad_flog = 0;
     for (size_t r = 0; r < nr; ++r) {
         const double* q = &J[9 * r];
         const unsigned long u = (unsigned long)q[0], n = (unsigned long)q[1];
@@ -53,6 +54,34 @@ int main(int argc, char** argv) {
             else if (in_range && eb >= LO && eb <= HI && eb > ea * (1.0 + 0x1p-48)) full = -1.0;
             else if (in_range && ea >= LO && ea <= HI && ea > eb * (1.0 + 0x1p-48)) full = 1.0;
             else full = ea / z / theta - eb / z / theta;
+            {  // (r06) the single-precision-log decision, with logf perturbed by up to 4 float ulps either way
+                const double za = x * alpha;
+                if (za >= 0x1p-29 && za <= 0x1p29 && theta >= 0x1p-30 && theta <= 0x1p30) {
+                    for (int pert = -4; pert <= 4; pert += 4) {
+                        float l2 = std::log2((float)za);
+                        for (int q = 0; q < (pert < 0 ? -pert : pert); ++q) l2 = std::nextafter(l2, pert < 0 ? -1e30f : 1e30f);
+                        const double lza = (double)l2 * 0.6931471805599453;
+                        const double alz = std::fabs(lza);
+                        const double Aa = nu_m * lza - za - lg_m, Ba = nu_a * lza - za - lg_a;
+                        const double S = nu_a * (alz + 1.0) + za + std::fabs(lg_m) + std::fabs(lg_a) + 1.0;
+                        const double e = 0x1p-17 * nu_a * (1.0 + alz) + 0x1p-46 * S;
+                        double dec = 2.0;
+                        if (e < 1.0) {
+                            if (Aa + e < -745.2 && Ba + e < -745.2) dec = 0.0;
+                            else {
+                                const double hi = Aa > Ba ? Aa : Ba;
+                                if (hi >= -650.0 && hi <= 650.0) {
+                                    const double d = Ba - Aa;
+                                    if (d > 0x1p-40 + e) dec = -1.0;
+                                    else if (-d > 0x1p-40 + e) dec = 1.0;
+                                }
+                            }
+                        }
+                        if (pert == 0) { if (dec != 2.0) ++flog_decided; else ++flog_fallback; }
+                        if (dec != 2.0 && dec != (skip != 2.0 ? skip : full)) ++bad_flog;
+                    }
+                }
+            }
             if (skip != 2.0) {
                 ++exp_skipped;
                 if (skip != full) ++bad_skip;
@@ -119,5 +148,7 @@ int main(int argc, char** argv) {
            "surrogate evaluations decided by the exp arguments %ld (differing from the exps' decision: %ld), by the exps "
            "without the divisions %ld, with the divisions %ld\n",
            nr, checked, bad_sign, bad_group[2], bad_group[3], exp_skipped, bad_skip, fast, slow);
-    return (bad_sign || bad_group[2] || bad_group[3] || bad_skip) ? 1 : 0;
+    printf("single-precision-log decisions: %ld decided, %ld left to the full path, %ld differing (logf exact and "
+           "perturbed by 4 float ulps either way)\n", flog_decided, flog_fallback, bad_flog);
+    return (bad_sign || bad_group[2] || bad_group[3] || bad_skip || bad_flog) ? 1 : 0;
 }
