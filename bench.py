@@ -51,8 +51,8 @@ STACKS = {
     #        kernel name)
     "pt_gs_k": (40, 16, 2 * 9 * 8, "ptgsk_run_kernel"),      # T P WS RH RAD in; discharge, charge out; 9 state
     "hbv_stack": (32, 16, 2 * 22 * 8, "hbv_run_kernel"),     # wind not read (hbv_stack.h:295-301); 22 state
-    "pt_ss_k": (40, 16, 2 * 8 * 8, "ptssk_run_kernel"),      # T P WS RH RAD in (WS unused by skaugen); 8 state
-    "pt_hs_k": (40, 16, 2 * 20 * 8, "pthsk_run_kernel"),     # T P WS RH RAD in; 20 state (hbv_snow bins + q)
+    "pt_ss_k": (32, 16, 2 * 8 * 8, "ptssk_run_kernel"),      # T P RH RAD in (wind not read: skaugen does not use it); 8 state
+    "pt_hs_k": (32, 16, 2 * 20 * 8, "pthsk_run_kernel"),     # T P RH RAD in (no wind: hbv_snow); 20 state (bins + q)
     "pt_hps_k": (40, 16, 2 * 37 * 8, "pthpsk_run_kernel"),   # T P WS RH RAD in; 37 state (hps bins + q)
 }
 

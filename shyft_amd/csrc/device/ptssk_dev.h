@@ -90,45 +90,18 @@ __device__ inline double ss_c(uint64_t n, double d_range) { return dexp(-(double
 // the test below would return -1 (or +1 with A and B swapped). And detmath's exp is exactly 0 below
 // -745.1332191019412 (exp_general), so two arguments below it are the underflow case. Of the bisection midpoints of
 // the year's 1M recorded jobs, 87 % are decided by the arguments and 11 % underflow; every decision agrees with the
-// full evaluation (tools/mb/ptssk_group_emu.cpp).
+// full evaluation (tools/mb/ptssk_group_emu.cpp). (A single-precision log in front of this, deciding 93 % of the
+// midpoints without the division and the double log, measured 1 % slower: a wavefront runs the full path whenever
+// one of its lanes needs it, and the remaining 2.5 % -- pdfs near the bottom of the double range -- are spread over
+// the jobs; profiles/r06/ptssk_flog_variant.txt.)
 #ifndef SHYFT_PTSSK_EXP_SKIP
 #define SHYFT_PTSSK_EXP_SKIP 1
 #endif
-// r06: and before any of that, the same decisions from a single-precision log and no division, wherever the margin
-// covers that estimate's error (else the full path below). z is estimated by x * alpha (theta = 1 / alpha rounded:
-// within 2^-50 relative of x / theta) and ln z by v_log_f32 (within 2^-19 (1 + |ln z|) here, far wider than its
-// 1-ulp specification); A and B by the same expressions on the estimates. With S bounding every intermediate, the
-// full path's A and B are within 2^-18 nu_a (1 + |ln z|) + 2^-49 S of the estimates, and `err` is twice that, so
-// d > 2^-40 + err gives B - A > 2^-40 (as for pdf_a's side), max within 650 gives max(A, B) within 660, and
-// estimates below -745.2 - err give arguments below exp's zero threshold: every decision here is one the exp-argument
-// test above would take.
-#ifndef SHYFT_PTSSK_FLOG_SIGN
-#define SHYFT_PTSSK_FLOG_SIGN 0
-#endif
-__device__ __forceinline__ double ss_zero_sign(double nu_m, double nu_a, double theta, double alpha, double lg_m,
-                                               double lg_a, double x, int32_t& err) {
+__device__ __forceinline__ double ss_zero_sign(double nu_m, double nu_a, double theta, double lg_m, double lg_a,
+                                               double x, int32_t& err) {
     if (x == 0) {
         const ss_pdf_pair f = ss_gamma_pdf2(nu_m, nu_a, theta, lg_m, lg_a, x, err);
         return f.m - f.a;
-    }
-    if (SHYFT_PTSSK_FLOG_SIGN) {
-        const double za = x * alpha;
-        if (za >= 0x1p-29 && za <= 0x1p29 && theta >= 0x1p-30 && theta <= 0x1p30) {
-            const double lza = (double)__builtin_amdgcn_logf((float)za) * 0.6931471805599453;
-            const double alz = fabs(lza);
-            const double Aa = nu_m * lza - za - lg_m, Ba = nu_a * lza - za - lg_a;
-            const double S = nu_a * (alz + 1.0) + za + fabs(lg_m) + fabs(lg_a) + 1.0;
-            const double e = 0x1p-17 * nu_a * (1.0 + alz) + 0x1p-46 * S;
-            if (e < 1.0) {
-                if (Aa + e < -745.2 && Ba + e < -745.2) return 0.0;
-                const double hi = Aa > Ba ? Aa : Ba;
-                if (hi >= -650.0 && hi <= 650.0) {
-                    const double d = Ba - Aa;
-                    if (d > 0x1p-40 + e) return -1.0;
-                    if (-d > 0x1p-40 + e) return 1.0;
-                }
-            }
-        }
     }
     const double z = x / theta;
     const double lz = dlog(z);
@@ -309,7 +282,7 @@ __device__ __forceinline__ double ss_sca_rel_red_body(uint64_t u, uint64_t n, do
             if (!G || L < 4) {
                 while (go_on()) {
                     const double mid = (bmin + bmax) / 2;
-                    const double fmid = ss_zero_sign(nu_m, nu_a, theta, alpha, lg_m, lg_a, mid, err);
+                    const double fmid = ss_zero_sign(nu_m, nu_a, theta, lg_m, lg_a, mid, err);
                     if ((mid == bmax) || (mid == bmin)) break;
                     if (fmid == 0) {
                         bmin = bmax = mid;
@@ -338,7 +311,7 @@ __device__ __forceinline__ double ss_sca_rel_red_body(uint64_t u, uint64_t n, do
                         if ((h >> b) & 1) lo = m2; else hi = m2;
                     }
                     int32_t e_spec = 0;  // raised below for the points the sequential loop evaluates
-                    const double fk = ss_zero_sign(nu_m, nu_a, theta, alpha, lg_m, lg_a, (lo + hi) / 2, e_spec);
+                    const double fk = ss_zero_sign(nu_m, nu_a, theta, lg_m, lg_a, (lo + hi) / 2, e_spec);
                     int node = 1;
                     for (int lev = 0; lev < D; ++lev) {
                         if (lev > 0 && !go_on()) {

@@ -20,6 +20,7 @@
 
 #include "../device/ptgsk_dev.h"
 #include "../device/gs_brent.h"
+#include "../device/stream.h"
 #include "../device/wave_place.h"
 #include "../include_internal/kernels.h"
 
@@ -48,21 +49,13 @@ extern "C" int shyft_ptgsk_prof_read(unsigned long long* out) {
 
 namespace {
 
-// forcing loads / response stores with the nontemporal hint (variant knob): the stream then does not displace the
-// step loop's scratch lines (register spills) from L2
+// forcing loads / response stores with the nontemporal hint (device/stream.h). r06, 1M cells, the year in 730-step
+// chunks: 74.0 -> 73.1 ms per chunk, January HBM traffic 1.84x -> 1.33x the algorithmic bytes
+// (profiles/r06/ptgsk_nt_variants.txt, tools/traffic_variants.sh)
 #ifndef SHYFT_PTGSK_NT
-#define SHYFT_PTGSK_NT 0
+#define SHYFT_PTGSK_NT 1
 #endif
-template <class T>
-__device__ __forceinline__ T f_ld(const T* p) {
-    if (SHYFT_PTGSK_NT) return __builtin_nontemporal_load(p);
-    return *p;
-}
-template <class T>
-__device__ __forceinline__ void r_st(T* p, T v) {
-    if (SHYFT_PTGSK_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+constexpr bool STREAM_NT = SHYFT_PTGSK_NT != 0;
 
 // (128- and 512-lane workgroups measured 7 % and 4 % slower over the year, r05)
 constexpr int BLOCK = 256;
@@ -220,11 +213,11 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
         const size_t ff = ENS ? wi * NF + fcl : fo;
         double temp = 0, rad = 0, rel_hum = 0, prec = 0, wind_speed = 0;
         if (valid) {
-            temp = f_ld(&f_temp[ff]);
-            rad = f_ld(&f_rad[ff]);
-            rel_hum = f_ld(&f_rh[ff]);
-            prec = f_ld(&f_prec[ff]) * p_corr;
-            wind_speed = f_ld(&f_ws[ff]);
+            temp = stream_ld<STREAM_NT && !ENS>(&f_temp[ff]);
+            rad = stream_ld<STREAM_NT && !ENS>(&f_rad[ff]);
+            rel_hum = stream_ld<STREAM_NT && !ENS>(&f_rh[ff]);
+            prec = stream_ld<STREAM_NT && !ENS>(&f_prec[ff]) * p_corr;
+            wind_speed = stream_ld<STREAM_NT && !ENS>(&f_ws[ff]);
             if (SS) collect_state(wi);
         }
         const bool start_melt = a.doy[i] == wed;
@@ -337,8 +330,8 @@ __global__ __launch_bounds__(B, WAVES) void ptgsk_run_kernel(const ptgsk_kargs a
                                   (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
         // collectors (pt_gs_k_cell_model.h:80-89, 116-124) of response.scale_snow(snow_storage_fraction)
-        r_st(&R[0 * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
-        r_st(&R[1 * RS + fo], charge_m3s);
+        stream_st<STREAM_NT>(&R[0 * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        stream_st<STREAM_NT>(&R[1 * RS + fo], charge_m3s);
         if (a.collect >= 1) {
             R[2 * RS + fo] = gs_sca;
             R[3 * RS + fo] = gs_storage * snow_storage_fraction;

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../device/stream.h"
 #include "../device/hps_dev.h"
 #include "../device/pt_dev.h"
 #include "../device/ptgsk_dev.h"
@@ -21,6 +22,13 @@
 using namespace shyft_dev;
 
 namespace {
+
+// forcing loads / response stores with the nontemporal hint (device/stream.h). r06, 1M cells, the year:
+// 63.3 -> 62.2 ms per 730-step chunk (profiles/r06/pthsk_pthpsk_nt_variants.txt), bit-exact
+#ifndef SHYFT_PTHPSK_NT
+#define SHYFT_PTHPSK_NT 1
+#endif
+constexpr bool STREAM_NT = SHYFT_PTHPSK_NT != 0;
 
 constexpr int BLOCK = 256;
 
@@ -153,11 +161,11 @@ void pthpsk_run_kernel(const pthpsk_kargs a) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
         const size_t ff = wi * NF + fcl;
-        const double temp = f_temp[ff];
-        const double rad = f_rad[ff];
-        const double rel_hum = f_rh[ff];
-        const double prec = f_prec[ff] * p_corr;
-        const double wind_speed = f_ws[ff];
+        const double temp = stream_ld<STREAM_NT>(&f_temp[ff]);
+        const double rad = stream_ld<STREAM_NT>(&f_rad[ff]);
+        const double rel_hum = stream_ld<STREAM_NT>(&f_rh[ff]);
+        const double prec = stream_ld<STREAM_NT>(&f_prec[ff]) * p_corr;
+        const double wind_speed = stream_ld<STREAM_NT>(&f_ws[ff]);
         if (SS) collect_state(wi);
         double r_sca, r_storage;
         const double snow_outflow = hps_step(hp, sp, sw, alb, iso, swe, sca, surface_heat, dt_us, dts, temp, rad, prec,
@@ -181,8 +189,8 @@ void pthpsk_run_kernel(const pthpsk_kargs a) {
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
         // all_response_collector of response.scale_snow(snow_storage_fraction) (pt_hps_k_cell_model.h:82-91,
         // pt_hps_k.h:196-202): hps_outflow is collected in mm/h, as the reference does
-        R[PR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
-        R[PR_CHARGE_M3S * RS + fo] = charge_m3s;
+        stream_st<STREAM_NT>(&R[PR_AVG_DISCHARGE * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        stream_st<STREAM_NT>(&R[PR_CHARGE_M3S * RS + fo], charge_m3s);
         if (a.collect >= 1) {
             R[PR_SNOW_SCA * RS + fo] = r_sca;
             R[PR_SNOW_SWE * RS + fo] = r_storage * snow_storage_fraction;

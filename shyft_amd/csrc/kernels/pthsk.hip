@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../device/stream.h"
 #include "../device/hbv_dev.h"
 #include "../device/pt_dev.h"
 #include "../device/ptgsk_dev.h"
@@ -24,6 +25,13 @@
 using namespace shyft_dev;
 
 namespace {
+
+// forcing loads / response stores with the nontemporal hint (device/stream.h). r06, 1M cells, the year:
+// 31.7 -> 31.5 ms per 730-step chunk (profiles/r06/pthsk_pthpsk_nt_variants.txt), bit-exact
+#ifndef SHYFT_PTHSK_NT
+#define SHYFT_PTHSK_NT 1
+#endif
+constexpr bool STREAM_NT = SHYFT_PTHSK_NT != 0;
 
 constexpr int BLOCK = 256;
 
@@ -126,10 +134,10 @@ void pthsk_run_kernel(const pthsk_kargs a) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
         const size_t ff = wi * NF + fcl;
-        const double temp = f_temp[ff];
-        const double rad = f_rad[ff];
-        const double rel_hum = f_rh[ff];
-        const double prec = f_prec[ff] * p_corr;
+        const double temp = stream_ld<STREAM_NT>(&f_temp[ff]);
+        const double rad = stream_ld<STREAM_NT>(&f_rad[ff]);
+        const double rel_hum = stream_ld<STREAM_NT>(&f_rh[ff]);
+        const double prec = stream_ld<STREAM_NT>(&f_prec[ff]) * p_corr;
         if (SS) collect_state(wi);
         const double snow_outflow = hbv_snow_step(sp_par, sp, sw, swe, sca, a.step_in_days, a.dt_hours, prec, temp, err);
         // glacier_melt::step (glacier_melt.h:47-52) on the post-step snow covered area
@@ -153,8 +161,8 @@ void pthsk_run_kernel(const pthsk_kargs a) {
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
         // collectors of response.scale_snow(snow_storage_fraction) (pt_hs_k.h:188-194, 274-277): the response
         // carries the post-step snow state, swe and outflow scaled
-        R[PR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
-        R[PR_CHARGE_M3S * RS + fo] = charge_m3s;
+        stream_st<STREAM_NT>(&R[PR_AVG_DISCHARGE * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        stream_st<STREAM_NT>(&R[PR_CHARGE_M3S * RS + fo], charge_m3s);
         if (a.collect >= 1) {
             R[PR_SNOW_SCA * RS + fo] = sca;
             R[PR_SNOW_SWE * RS + fo] = swe * snow_storage_fraction;

@@ -40,6 +40,7 @@ extern "C" int shyft_ptssk_prof_read(unsigned long long* out) {
 #include "../device/pt_dev.h"
 #include "../device/ptgsk_dev.h"
 #include "../device/ptssk_dev.h"
+#include "../device/stream.h"
 #include "../device/wave_place.h"
 #include "../include_internal/kernels.h"
 
@@ -58,6 +59,14 @@ using namespace shyft_dev;
 namespace {
 
 constexpr int BLOCK = 256;
+
+// forcing loads / response stores with the nontemporal hint (device/stream.h). r06, 1M cells, the year in 730-step
+// chunks: 73.6 -> 72.6 ms per chunk, April HBM traffic 2.33x -> 1.41x the algorithmic bytes
+// (profiles/r06/ptssk_nt_variants.txt)
+#ifndef SHYFT_PTSSK_NT
+#define SHYFT_PTSSK_NT 1
+#endif
+constexpr bool STREAM_NT = SHYFT_PTSSK_NT != 0;
 
 // occupancy target (waves per SIMD; variant builds override with -DSHYFT_PTSSK_WAVES=N)
 #ifndef SHYFT_PTSSK_WAVES
@@ -213,10 +222,10 @@ void ptssk_run_kernel(const ptssk_kargs a) {
         const size_t wi = (size_t)(i - a.win0);
         const size_t fo = wi * N + cell;
         const size_t ff = wi * NF + fcl;
-        const double temp = f_temp[ff];
-        const double rad = f_rad[ff];
-        const double rel_hum = f_rh[ff];
-        const double prec = f_prec[ff] * p_corr;
+        const double temp = stream_ld<STREAM_NT>(&f_temp[ff]);
+        const double rad = stream_ld<STREAM_NT>(&f_rad[ff]);
+        const double rel_hum = stream_ld<STREAM_NT>(&f_rh[ff]);
+        const double prec = stream_ld<STREAM_NT>(&f_prec[ff]) * p_corr;
         if (SS && valid) collect_state(wi);
         double snow_outflow = 0, snow_sca = 0, snow_swe = 0;
         ss_mid m;
@@ -307,8 +316,8 @@ void ptssk_run_kernel(const ptssk_kargs a) {
                                   (cell_area_m2 * ae * mmh_to_m3s_scale_factor) + gm_melt_m3s -
                                   (cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
         // collectors of response.scale_snow(snow_storage_fraction) (pt_ss_k.h:198-203)
-        R[PR_AVG_DISCHARGE * RS + fo] = cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor;
-        R[PR_CHARGE_M3S * RS + fo] = charge_m3s;
+        stream_st<STREAM_NT>(&R[PR_AVG_DISCHARGE * RS + fo], cell_area_m2 * total_discharge * mmh_to_m3s_scale_factor);
+        stream_st<STREAM_NT>(&R[PR_CHARGE_M3S * RS + fo], charge_m3s);
         if (a.collect >= 1) {
             R[PR_SNOW_SCA * RS + fo] = snow_sca;
             R[PR_SNOW_SWE * RS + fo] = snow_swe * snow_storage_fraction;
