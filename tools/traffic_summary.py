@@ -16,6 +16,7 @@ stack = sys.argv[3] if len(sys.argv) > 3 else "pt_gs_k"
 kern, state_b, step_b = {"pt_gs_k": ("ptgsk_run_kernel", 144.0, 56.0), "pt_ss_k": ("ptssk_run_kernel", 128.0, 48.0)}[stack]
 f = counter_rows(os.path.join(d, f"{n}_FETCH_SIZE", "run_counter_collection.csv"), kern)
 w = counter_rows(os.path.join(d, f"{n}_WRITE_SIZE", "run_counter_collection.csv"), kern)
+tot_t = tot_a = 0.0
 for k, ((_, fr, fm), (_, wr, wm)) in enumerate(zip(f, w)):
     steps = 730
     alg = fm["grid"] * (step_b * steps + state_b)
@@ -24,3 +25,6 @@ for k, ((_, fr, fm), (_, wr, wm)) in enumerate(zip(f, w)):
     print(f"{n:12s} launch {k}: fetch {fb / 1e9:6.2f} GB  write {wb / 1e9:6.2f} GB  traffic/algorithmic "
           f"{(fb + wb) / alg:5.2f}  ({fm['duration_ns'] / 1e6:.1f} / {wm['duration_ns'] / 1e6:.1f} ms, scratch "
           f"{fm['scratch_bytes_per_lane']} B/lane)", flush=True)
+    tot_t += fb + wb
+    tot_a += alg
+print(f"{n:12s} all launches: traffic/algorithmic {tot_t / tot_a:5.3f}", flush=True)
