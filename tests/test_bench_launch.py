@@ -67,6 +67,39 @@ def test_first_attempt_line_carries_supervisor_field():
     assert out["supervisor"]["attempt"] == 0 and out["supervisor"]["previous_attempt"] is None
 
 
+def _torchrun(world, args, env_extra=None, timeout=300):
+    """The driver's N > 1 command: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
+    127.0.0.1 --master-port P bench.py --gpus N ... (torchrun's agent hosts the store the supervisors share)."""
+    from shyft_amd.supervise import _free_port
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world)] + args
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p, (json.loads(lines[-1]) if lines else None)
+
+
+def test_torchrun_gloo_dist_check():
+    p, out = _torchrun(2, ["--dist-check", "--total-cells", "4096"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["n_gpus"] == 2 and out["max_abs_diff"] < 1e-9 and out["supervisor"]["attempt"] == 0
+    assert len([l for l in p.stdout.splitlines() if l.startswith("{")]) == 1
+
+
+def test_torchrun_stalled_self_check_restarts_ranks_with_host_combines():
+    """The same stall as above under torch.distributed.run: the supervisors agree over torchrun's agent store."""
+    p, out = _torchrun(2, ["--dist-check", "--total-cells", "4096"],
+                       env_extra={"SHYFT_DIST_TEST_STALL": "1:0", "SHYFT_SUPERVISE_STALL_S": "6",
+                                  "SHYFT_SUPERVISE_FIRST_S": "120", "SHYFT_DIST_TIMEOUT_S": "60"}, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert out is not None and out["max_abs_diff"] < 1e-9
+    assert out["supervisor"]["attempt"] == 1 and out["supervisor"]["combines"] == "gloo"
+
+
 def test_world_size_mismatch_fails():
     p, out = _bench(["--gpus", "2", "--dist-check"], env_extra={"WORLD_SIZE": "3", "RANK": "0"})
     assert p.returncode != 0 and out is None
@@ -90,6 +123,20 @@ def test_two_ranks_one_gpu_catchment_sums_match_single_rank(stack, tmp_path):
     s1, s2 = np.load(tmp_path / "s1.npy"), np.load(tmp_path / "s2.npy")
     assert s1.shape == (100, 144) and np.isfinite(s1).all() and s1.sum() > 0
     assert np.array_equal(s1, s2)
+
+
+@pytest.mark.gpu
+def test_torchrun_two_ranks_one_gpu_match_single_rank(tmp_path):
+    """The driver's launcher (torch.distributed.run) over the real GPU bench: two supervised ranks on one device
+    (gloo combines: RCCL cannot hold two ranks of one communicator on one device) give the single rank's sums."""
+    common = ["--total-cells", "4096", "--catchments", "100", "--chunk", "48", "--steps", "3", "--warmup", "0",
+              "--no-cpu-baseline"]
+    p1, o1 = _bench(["--gpus", "1", "--dump-sums", str(tmp_path / "s1.npy")] + common)
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    p2, o2 = _torchrun(2, ["--dump-sums", str(tmp_path / "s2.npy")] + common, env_extra={"SHYFT_DIST_BACKEND": "gloo"})
+    assert p2.returncode == 0, p2.stderr[-2000:]
+    assert o2["n_gpus"] == 2 and o2["supervisor"]["attempt"] == 0
+    assert np.array_equal(np.load(tmp_path / "s1.npy"), np.load(tmp_path / "s2.npy"))
 
 
 @pytest.mark.gpu
