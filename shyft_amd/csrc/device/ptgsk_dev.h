@@ -530,10 +530,11 @@ __device__ inline bool kirchner_step(double& q, double& q_avg, double p, double 
         }
     }
     // calc_state(t1): dopri5 continuous extension
-    {
+    struct ext_coeffs {
+        double b1, b3, b4, b5, b6, b7;
+    };
+    auto coeffs = [](double theta) {
         const double b1 = 35.0 / 384, b3 = 500.0 / 1113, b4 = 125.0 / 192, b5 = -2187.0 / 6784, b6 = 11.0 / 84;
-        const double h = t - t_old;
-        const double theta = (t1 - t_old) / h;
         const double X1 = 5.0 * (2558722523.0 - 31403016.0 * theta) / 11282082432.0;
         const double X3 = 100.0 * (882725551.0 - 15701508.0 * theta) / 32700410799.0;
         const double X4 = 25.0 * (443332067.0 - 31403016.0 * theta) / 1880347072.0;
@@ -546,18 +547,33 @@ __device__ inline bool kirchner_step(double& q, double& q_avg, double p, double 
         const double B = theta_sq * theta_m_1;
         const double C = theta_sq * theta_m_1 * theta_m_1;
         const double D = theta * theta_m_1 * theta_m_1;
-        const double b1_theta = A * b1 - C * X1 + D;
-        const double b3_theta = A * b3 + C * X3;
-        const double b4_theta = A * b4 - C * X4;
-        const double b5_theta = A * b5 + C * X5;
-        const double b6_theta = A * b6 - C * X6;
-        const double b7_theta = B + C * X7;
-        x = 1.0 * x_old + h * b1_theta * dxdt_old + h * b3_theta * k3 + h * b4_theta * k4 + h * b5_theta * k5 +
-            h * b6_theta * k6 + h * b7_theta * dxdt;
-    }
+        ext_coeffs c;
+        c.b1 = A * b1 - C * X1 + D;
+        c.b3 = A * b3 + C * X3;
+        c.b4 = A * b4 - C * X4;
+        c.b5 = A * b5 + C * X5;
+        c.b6 = A * b6 - C * X6;
+        c.b7 = B + C * X7;
+        return c;
+    };
+    const double h = t - t_old;
+    // the usual hour: one accepted step from 0 to t1, so theta = (t1 - 0) / t1 = 1 exactly, and the coefficients are
+    // the same IEEE operations on the constant 1.0 -- folded at compile time: six divisions and the rest of the
+    // polynomial algebra fewer per call (the oracle evaluates them at run time, with the same bits). The weighted sum
+    // is written out in each branch (one value joins, not six coefficients: fewer registers live at the join).
+    // r06, 1M cells, the year in 730-step chunks: pt_gs_k 72.9 -> 70.8 ms, pt_ss_k 72.6 -> 70.3 (with the coefficients
+    // joined instead: 71.5 / 70.9; profiles/r06/kirchner_extension_variants.txt)
+    auto sum = [&](const ext_coeffs& c) {
+        return 1.0 * x_old + h * c.b1 * dxdt_old + h * c.b3 * k3 + h * c.b4 * k4 + h * c.b5 * k5 + h * c.b6 * k6 +
+               h * c.b7 * dxdt;
+    };
+    if (t_old == 0.0 && h == t1 && t1 > 0.0 && t1 <= 1.7976931348623157e308)
+        x = sum(coeffs(1.0));
+    else
+        x = sum(coeffs((t1 - t_old) / h));
     q = dexp(x);
     area += 0.5 * (f_a + q) * (t1 - t_a);
-    q_avg = area / (t1 - 0.0);
+    q_avg = t1 == 1.0 ? area : area / (t1 - 0.0);  // x / 1.0 == x exactly (hourly steps)
     return ok;
 }
 
