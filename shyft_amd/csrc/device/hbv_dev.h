@@ -185,7 +185,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par_t<NB>& p, double (&sp)
         for (int i = 0; i < NB; ++i) sp[i] = sw[i] = 0.0;
         s_swe = 0.0;
         s_sca = 0.0;
-        return total_water / dt_hours;
+        return dt_hours == 1.0 ? total_water : total_water / dt_hours;  // x / 1.0 == x exactly (hourly steps)
     }
     if (snow > 0.0) {
         int idx = nb - 1;  // sca_index (hbv_snow.h:175-180)
@@ -277,7 +277,7 @@ __device__ inline double hbv_snow_step(const hbv_snow_par_t<NB>& p, double (&sp)
     }
     s_swe = swe;
     s_sca = sca;
-    return (total_water - swe) / dt_hours;
+    return dt_hours == 1.0 ? total_water - swe : (total_water - swe) / dt_hours;  // as above
 }
 
 }  // namespace shyft_dev

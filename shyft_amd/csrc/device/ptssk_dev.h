@@ -436,7 +436,8 @@ __device__ inline void ss_front(const ss_par& p, double step_in_days, double dt_
     m.need = false;
 
     if (s.sca * s.swe < unit_size && snow < snow_tol) {
-        r_outflow = (rain + s.sca * (s.swe + s.free_water) + s.residual) / dt_hours;
+        r_outflow = rain + s.sca * (s.swe + s.free_water) + s.residual;
+        if (dt_hours != 1.0) r_outflow = r_outflow / dt_hours;  // x / 1.0 == x exactly (hourly steps)
         s.residual = 0.0;
         if (r_outflow < 0.0) {
             s.residual = r_outflow;
@@ -559,7 +560,7 @@ __device__ inline void ss_back(const ss_par& p, double dt_hours, ss_state& s, co
     }
     // 5. state and response
     if (nnn > 0) nu /= (double)nnn;
-    r_outflow = discharge / dt_hours;
+    r_outflow = dt_hours == 1.0 ? discharge : discharge / dt_hours;  // as in ss_front
     r_swe = sca * (swe + lwc);
     r_sca = sca;
     s.nu = nu;
