@@ -45,6 +45,7 @@ METRIC = "cell-steps/sec (cells×timesteps/wall) for pt_gs_k at 1/2/4/8 MI355X"
 CHUNK = 438                      # 20 chunks = one calendar year (8760 hourly steps)
 YEAR = 8760
 HBM_PEAK_BPS = 8.0e12            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SMALL_REGION_CELLS = 2 * 256 * 256   # cells per GPU at which a 256-lane launch gives each CU at most 2 workgroups
 # algorithmic HBM bytes of the dominant kernel
 STACKS = {
     # name: (forcing bytes read per cell-step, series bytes written per cell-step, state bytes per cell per launch,
@@ -100,9 +101,11 @@ def parse(argv=None):
     ap.add_argument("--pipeline", action="store_true",
                     help="two regions: generate chunk s+1's forcing while chunk s runs (measured slower for pt_gs_k, "
                          "see DESIGN.md section 5; off by default)")
-    ap.add_argument("--overlap-forcing", type=int, default=0, metavar="CUS",
-                    help="generate chunk s+1's forcing into a second window buffer on a side stream of CUS CUs while "
-                         "chunk s runs (0: generate each chunk before its run)")
+    ap.add_argument("--overlap-forcing", type=int, default=None, metavar="CUS",
+                    help="generate chunk s+1's forcing into a second window buffer on a side stream while chunk s "
+                         "runs: CUS > 0 CUs, or -1 the whole device at the lowest stream priority (0: generate each "
+                         "chunk before its run). Default: -1 for a region too small to fill the GPU (<= 131,072 "
+                         "cells per GPU), else 0")
     ap.add_argument("--chunk", type=int, default=CHUNK)
     ap.add_argument("--cpu-cells", type=int, default=4000, help="cpu_baseline sample cells (x 8760 steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os cpu share)")
@@ -479,9 +482,11 @@ def _sync():
 
 def _run_year_overlapped(r, L, chunk, k_steps, seed, router, sums, walls, parts, n_cus):
     """As run_year with the device generator, but chunk s+1's forcing is generated into the region's second window
-    buffer on a side stream of n_cus CUs while chunk s runs (shyft_hip_prefetch_synthetic_forcing), and the buffers
-    swap before chunk s+1 (the run waits for the generator on the device). Chunk 0's forcing is generated before
-    its run, inside the timed region like every other chunk's."""
+    buffer on a side stream while chunk s runs (shyft_hip_prefetch_synthetic_forcing), and the buffers swap before
+    chunk s+1 (the run waits for the generator on the device). n_cus > 0: the side stream is restricted to that many
+    CUs; n_cus < 0: the whole device at the lowest stream priority, enqueued after chunk s's run, so the run's
+    workgroups are dispatched first and the generator's fill the CUs its tail leaves idle. Chunk 0's forcing is
+    generated before its run, inside the timed region like every other chunk's."""
     kernel_ms = []
     r.move_window(0, 0)
     r.synthetic_forcing(seed, 0, chunk, cell_offset=L.off)
@@ -489,9 +494,15 @@ def _run_year_overlapped(r, L, chunk, k_steps, seed, router, sums, walls, parts,
         _progress(f"chunk {s}")
         t_chunk = time.perf_counter()
         step0 = s * chunk
-        if s + 1 < k_steps:
-            r.prefetch_synthetic_forcing(seed, step0 + chunk, cell_offset=L.off, n_cus=n_cus)
-        r.run_cells(0, step0, chunk)
+        if n_cus < 0:
+            r.run_cells_async(step0, chunk)
+            if s + 1 < k_steps:
+                r.prefetch_synthetic_forcing(seed, step0 + chunk, cell_offset=L.off, n_cus=n_cus)
+            r.synchronize()   # the run's error check (region_model::run_cells semantics)
+        else:
+            if s + 1 < k_steps:
+                r.prefetch_synthetic_forcing(seed, step0 + chunk, cell_offset=L.off, n_cus=n_cus)
+            r.run_cells(0, step0, chunk)
         kernel_ms.append(r.last_run_ms())
         if parts is not None:
             parts.append(r.last_run_kernel_ms())
@@ -757,6 +768,12 @@ def main():
     n_dev = len(set(devices)) if devices else world
     L = Layout(a, world, rank, engine_gpus=n_dev if devices else 0)
     cells = L.total // n_dev if devices else L.n      # per GPU (the shards of one GPU run concurrently)
+    if a.overlap_forcing is None:
+        # a region of at most 2 workgroups per CU leaves the GPU under-filled: its next window's forcing is generated
+        # beside the run at the lowest stream priority (measured r06, 131,072 cells: 7.21e9 -> 7.38e9 cell-steps/s);
+        # a full region generates before its run (overlapping it slowed the 1M-cell run kernel 42.1 -> 48.1 ms,
+        # profiles/r06/forcing_overlap_variants.txt)
+        a.overlap_forcing = -1 if (cells <= SMALL_REGION_CELLS and not a.idw and not a.btk and not a.pipeline) else 0
     chunk = a.chunk
     n_axis = max(YEAR, (max(a.steps, a.warmup)) * chunk)
     from shyft_amd.region import SHARD_BALANCE_Z
@@ -839,8 +856,11 @@ def main():
             "catchments": L.n_catch,
             "steps_per_chunk": chunk,
             "forcing": ("IDW/BTK from stations, per chunk, before its run" if a.idw else
-                        f"device generator, chunk s+1 into a second window buffer on a {a.overlap_forcing}-CU side "
-                        "stream while chunk s runs (chunk 1 before its run)" if a.overlap_forcing else
+                        ("device generator, chunk s+1 into a second window buffer on a whole-device lowest-priority "
+                         "side stream enqueued after chunk s's run (chunk 1 before its run); every chunk's forcing is "
+                         "generated inside the timed region" if a.overlap_forcing < 0 else
+                         f"device generator, chunk s+1 into a second window buffer on a {a.overlap_forcing}-CU side "
+                         "stream while chunk s runs (chunk 1 before its run)") if a.overlap_forcing else
                         "device generator, per chunk, overlapped with the previous chunk's run (two regions, state "
                         "handed over device to device)" if r_alt is not None else
                         "device generator, per chunk, before its run"),

@@ -220,8 +220,9 @@ int shyft_hip_run_cells(shyft_hip_region* h, size_t use_ncore, int start_step, i
 int shyft_hip_run_cells_async(shyft_hip_region* h, int start_step, int n_steps);
 int shyft_hip_synchronize(shyft_hip_region* h);
 /* Double-buffered forcing window (measurement / pipelining aid, no reference counterpart): generate the synthetic
-   forcing of the window starting at w0_next into a second buffer on a side stream restricted to n_cus CUs (<= 0:
-   no restriction) while the current window runs; shyft_hip_swap_forcing_window(h, w0_next) then makes it the
+   forcing of the window starting at w0_next into a second buffer on a side stream restricted to n_cus CUs (0: no
+   restriction; < 0: the whole device at the lowest stream priority) while the current window runs (it waits only
+   for the run that last read that buffer); shyft_hip_swap_forcing_window(h, w0_next) then makes it the
    region's window (the next run waits for the generator on the device). The swap does not NaN-fill the response
    and state-series rows: a run over the new window must follow before they are read. A pending prefetch is
    dropped when the time axis or window length changes (shyft_hip_set_time_axis). */

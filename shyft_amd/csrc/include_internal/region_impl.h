@@ -95,6 +95,8 @@ struct shyft_hip_region {
     hipStream_t gen_stream = nullptr;
     int gen_cus = -1;
     hipEvent_t ev_gen = nullptr;
+    hipEvent_t ev_free = nullptr;  // recorded at the last swap: the swapped-out buffer's last reader has finished
+    bool free_pending = false;
     size_t gen_w0 = SIZE_MAX;
     dbuf<int32_t> d_set_ix, d_err, d_doy, d_seg_cells, d_seg_off, d_sel;
     dbuf<int64_t> d_trel;

@@ -249,6 +249,7 @@ void update_derived(shyft_hip_region* h) {
 void cancel_prefetch(shyft_hip_region* h) {
     if (h->gen_stream) hip_check(hipStreamSynchronize(h->gen_stream), "sync generator");
     h->gen_w0 = SIZE_MAX;
+    h->free_pending = false;
     h->d_forcing_next.release();
 }
 
@@ -432,6 +433,7 @@ void shyft_hip_region_destroy(shyft_hip_region* h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->ev_gen) (void)hipEventDestroy(h->ev_gen);
+    if (h->ev_free) (void)hipEventDestroy(h->ev_free);
     if (h->gen_stream) (void)hipStreamDestroy(h->gen_stream);
     if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -749,6 +751,13 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
                 }
                 hip_check(hipExtStreamCreateWithCUMask(&h->gen_stream, uint32_t(mask.size()), mask.data()),
                           "hipExtStreamCreateWithCUMask");
+            } else if (n_cus < 0) {
+                // the whole device at the lowest stream priority: the run kernel's workgroups (normal priority,
+                // launched first) are dispatched before the generator's, which fill the CUs its tail leaves idle
+                int least = 0, greatest = 0;
+                hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+                hip_check(hipStreamCreateWithPriority(&h->gen_stream, hipStreamNonBlocking, least),
+                          "hipStreamCreateWithPriority");
             } else {
                 hip_check(hipStreamCreateWithFlags(&h->gen_stream, hipStreamNonBlocking), "hipStreamCreate");
             }
@@ -756,9 +765,14 @@ int shyft_hip_prefetch_synthetic_forcing(shyft_hip_region* h, uint64_t seed, uin
         }
         if (!h->ev_gen) hip_check(hipEventCreateWithFlags(&h->ev_gen, hipEventDisableTiming), "hipEventCreate");
         h->d_forcing_next.alloc(h->d_forcing.n);
-        // the buffer was last read by a run on the region stream: the generator waits for that stream first
-        hip_check(hipEventRecord(h->ev_gen, h->stream), "record");
-        hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_gen, 0), "wait");
+        // the buffer was last read by a run on the region stream: the generator waits for that run -- the event the
+        // last swap recorded behind it, or else everything on the region stream so far
+        if (h->free_pending) {
+            hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_free, 0), "wait");
+        } else {
+            hip_check(hipEventRecord(h->ev_gen, h->stream), "record");
+            hip_check(hipStreamWaitEvent(h->gen_stream, h->ev_gen, 0), "wait");
+        }
         const int blocks = 4 * (n_cus > 0 ? n_cus : 256);  // 4 workgroups of 4 waves per CU (grid-stride over cells)
         hip_check(launch_synthetic_forcing_stream(h->d_forcing_next.p, h->TW, 0, h->TW, h->n, seed, cell_offset,
                                                   w0_next, h->d_alt.p, blocks, h->gen_stream, h->d_cell_ids.p),
@@ -780,6 +794,11 @@ int shyft_hip_swap_forcing_window(shyft_hip_region* h, size_t w0_next) {
         // error (shyft_hip.h)
         // later work on the region stream (the next run) waits for the generator, without a host wait
         hip_check(hipStreamWaitEvent(h->stream, h->ev_gen, 0), "wait generator");
+        // the buffer swapped out was read by the runs enqueued so far: the next prefetch into it waits for them only
+        // (not for the run enqueued after this swap, which reads the other buffer)
+        if (!h->ev_free) hip_check(hipEventCreateWithFlags(&h->ev_free, hipEventDisableTiming), "hipEventCreate");
+        hip_check(hipEventRecord(h->ev_free, h->stream), "record");
+        h->free_pending = true;
         std::swap(h->d_forcing.p, h->d_forcing_next.p);
         std::swap(h->d_forcing.n, h->d_forcing_next.n);
         h->w0 = w0_next;

@@ -165,15 +165,17 @@ def test_sharded_routing_matches_single_rank(world, cells, tmp_path):
 
 
 @pytest.mark.gpu
-def test_overlapped_forcing_generation_same_results(tmp_path):
-    """bench --overlap-forcing (chunk s+1's forcing generated into a second window buffer on a CU-restricted side
-    stream while chunk s runs, then swapped in) gives the same catchment sums as generating each chunk before its
-    run: the same generator, the same rows, the run waits for the generator on the device."""
+@pytest.mark.parametrize("cus", ["8", "-1"])
+def test_overlapped_forcing_generation_same_results(tmp_path, cus):
+    """bench --overlap-forcing (chunk s+1's forcing generated into a second window buffer on a side stream -- 8 CUs,
+    or the whole device at the lowest priority enqueued after chunk s's run -- then swapped in) gives the same
+    catchment sums as generating each chunk before its run: the same generator, the same rows, the run waits for the
+    generator on the device and the generator for the run that last read its buffer."""
     common = ["--total-cells", "20000", "--catchments", "50", "--chunk", "96", "--steps", "4", "--warmup", "1",
               "--no-cpu-baseline"]
     p0, o0 = _bench(["--dump-sums", str(tmp_path / "a.npy")] + common)
     assert p0.returncode == 0, p0.stderr[-2000:]
-    p1, o1 = _bench(["--dump-sums", str(tmp_path / "b.npy"), "--overlap-forcing", "8"] + common)
+    p1, o1 = _bench(["--dump-sums", str(tmp_path / "b.npy"), "--overlap-forcing", cus] + common)
     assert p1.returncode == 0, p1.stderr[-2000:]
     a, b = np.load(tmp_path / "a.npy"), np.load(tmp_path / "b.npy")
     assert a.shape == (50, 384) and np.isfinite(a).all() and a.sum() > 0
